@@ -1,0 +1,139 @@
+/*
+ * ptv_api.h — C ABI of the MI355X-native PTV scattered-to-grid interpolator.
+ *
+ * Drop-in boundary for the per-voxel neighbour search + weighted average of
+ * the reference `interpolator.interpolate_field` (tombultreys/ptv_interpolation,
+ * interpolator.py:65-203).  Plain C types only: pointers + sizes, no torch or
+ * HIP types in any signature.  Every entry point returns 0 on success and a
+ * negative PTV_E* code on failure; `ptv_last_error()` then holds a message
+ * (thread-local).  The Python mirror of the reference interface lives in
+ * ptv_interpolation_amd/interpolator.py and binds these symbols with ctypes.
+ *
+ * Threading: one ptv_ctx per (process, device).  A ctx is not re-entrant;
+ * calls on one ctx are synchronous with respect to the host unless the
+ * *_dev variant is given a stream, in which case all work is enqueued on
+ * that stream and the call returns after the enqueue (the stats fields
+ * are filled at the next synchronising call).
+ */
+#ifndef PTV_API_H
+#define PTV_API_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PTV_API_VERSION 1
+
+/* error codes */
+#define PTV_OK 0
+#define PTV_E_ARG -1      /* invalid argument (Python: ValueError)          */
+#define PTV_E_HIP -2      /* HIP runtime / launch failure (RuntimeError)    */
+#define PTV_E_NOMEM -3    /* device allocation failed (MemoryError)         */
+#define PTV_E_UNSUPPORTED -4 /* valid but not implemented on the GPU path  */
+#define PTV_E_INEXACT -5  /* a slab-culled particle set could not prove exactness */
+#define PTV_E_SINGULAR -6 /* local RBF system singular (Python: LinAlgError) */
+
+/* interpolation methods (interpolator.py:83, :126, :157, :197) */
+#define PTV_METHOD_IDW 0
+#define PTV_METHOD_SIBSON 1
+#define PTV_METHOD_NEAREST 2
+
+/* flags for ptv_knn_params.flags */
+#define PTV_FLAG_NAN_TO_NUM 1u  /* fused main.py:195-199 nan_to_num on the outputs */
+
+typedef struct ptv_ctx ptv_ctx;
+
+/*
+ * Particles, structure of arrays, float64 (the reference upcasts every input
+ * to float64: interpolator.py:78-79 -> cKDTree / numpy arithmetic).
+ * Replaces: `points = df[['x','y','z']].values; values = df[['u','v','w']].values`
+ *           (interpolator.py:78-79).
+ */
+typedef struct {
+    int64_t n;
+    const double *x, *y, *z; /* positions */
+    const double *u, *v, *w; /* velocity components */
+} ptv_particles;
+
+/*
+ * Query grid.  Separable regular grid: the 1-D axes returned by
+ * `create_grid` (interpolator.py:54-56) — voxel (iz, iy, ix) sits at
+ * (ax[ix], ay[iy], az[iz]), C order (nz, ny, nx) with x fastest exactly as
+ * `np.stack([X.ravel(), Y.ravel(), Z.ravel()], -1)` (interpolator.py:135).
+ * Point-list mode: ax/ay/az NULL and px/py/pz hold nx*ny*nz coordinates in
+ * the same C order (any grid shape the caller passes, interpolator.py:77).
+ * Only planes [z_begin, z_end) are computed (multi-GPU z-slab).
+ */
+typedef struct {
+    int64_t nx, ny, nz;
+    const double *ax, *ay, *az;
+    const double *px, *py, *pz;
+    int64_t z_begin, z_end;
+} ptv_grid;
+
+/*
+ * k-NN interpolation parameters (interpolate_field kwargs, interpolator.py:65).
+ * fluid_mask: optional uint8 (nz, ny, nx) over the FULL grid, nonzero = fluid
+ * (interpolator.py:37); solid voxels are written as 0 and skipped
+ * (fused main.py:202-207).  NULL = compute every voxel.
+ */
+typedef struct {
+    int method;          /* PTV_METHOD_* */
+    int k;               /* idw_neighbors / sibson_neighbors */
+    double power;        /* idw_power (interpolator.py:143) */
+    double eps;          /* 1e-10 (interpolator.py:102, :142) */
+    const uint8_t *fluid_mask;
+    uint32_t flags;      /* PTV_FLAG_* */
+    double cell_occupancy; /* target particles per binning cell, <=0: default */
+} ptv_knn_params;
+
+/* Per-call timings (ms, hipEvent based) and sizes. */
+typedef struct {
+    double ms_h2d, ms_bin, ms_knn, ms_d2h, ms_total;
+    int64_t n_particles, n_voxels, n_cells;
+    int32_t cells[3];
+    int32_t levels;
+    double cell_size[3];
+} ptv_stats;
+
+/* Library / device management. */
+int ptv_version(void);
+const char *ptv_last_error(void);
+int ptv_device_count(int *out);
+int ptv_init(int device, ptv_ctx **out);
+int ptv_free(ptv_ctx *ctx);
+
+/*
+ * k-NN IDW / Sibson interpolation, host buffers.
+ * Replaces the `method == 'idw'` branch (interpolator.py:126-155) and the
+ * `method == 'sibson'` branch (interpolator.py:83-124): KDTree build
+ * (:90,:132), query (:97,:139), weights (:102-116,:142-147), gather-sum
+ * (:119-122,:150-153), reshape (:124,:155,:199-203).
+ * Outputs U, V, W: caller-owned float64 (z_end-z_begin, ny, nx) C order.
+ */
+int ptv_interp_knn(ptv_ctx *ctx, const ptv_particles *p, const ptv_grid *g,
+                   const ptv_knn_params *prm, double *U, double *V, double *W,
+                   ptv_stats *st);
+
+/*
+ * Same, every pointer (particles, axes/points, mask, outputs) is DEVICE
+ * memory on the ctx's device; work is enqueued on `stream` (hipStream_t,
+ * NULL = the ctx's own stream) and the call returns after the enqueue.
+ */
+int ptv_interp_knn_dev(ptv_ctx *ctx, const ptv_particles *p, const ptv_grid *g,
+                       const ptv_knn_params *prm, double *U, double *V, double *W,
+                       void *stream, ptv_stats *st);
+
+/*
+ * Last-launch k-NN kernel duration in ms (hipEvent pair recorded around the
+ * kernel on the stream it ran on) and the synchronised phase stats.
+ */
+int ptv_last_stats(ptv_ctx *ctx, ptv_stats *st);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PTV_API_H */

@@ -1,0 +1,243 @@
+"""CPU restatement of the reference hot path — TEST INFRASTRUCTURE ONLY.
+
+This module is the *checker* for the MI355X k-NN interpolation path.  Only
+``tests/``, ``__graft_entry__.smoke()`` and the ``cpu_baseline`` leg of
+``bench.py`` may import it.  Nothing under ``ptv_interpolation_amd/`` imports
+it, and the shipped path never falls back to it.
+
+What it restates (reference = tombultreys/ptv_interpolation, read-only):
+
+* ``interpolator.interpolate_field`` IDW branch  (interpolator.py:126-155)
+* ``interpolator.interpolate_field`` Sibson branch (interpolator.py:83-124)
+* the RBF process fan-out pattern (interpolator.py:173-182,
+  test_parallel.py:6-28) as a z-slab ``ProcessPoolExecutor`` driver used as the
+  same-box CPU baseline.
+
+The k-NN search itself lives in the reference's third-party dependency
+``scipy.spatial.KDTree`` (cKDTree, unpinned in requirements.txt:2; this image
+ships scipy 1.15.3).  ``knn_kdtree`` calls it exactly as the reference does
+(interpolator.py:132,139).  ``knn_bruteforce`` is an independent numpy
+restatement of the same contract — Euclidean k nearest, ascending distance,
+``d = sqrt((dx*dx + dy*dy) + dz*dz)`` (the cKDTree p=2 accumulation order,
+verified bit-exact against cKDTree in this container) — used to cross-check
+the tree on small cases.
+
+Numerics pinned here (each verified bit-exact against numpy 2.2.6 in
+``tests/test_oracle.py``):
+
+* ``x.sum(axis=1)`` over a C-contiguous (V, k) array is ``0.0 + pairwise(row)``
+  where ``pairwise`` is numpy's 8-accumulator blocked pairwise summation
+  (``pairwise_sum`` below).
+* ``d ** p`` takes numpy's scalar fast paths: p=2 -> d*d, p=1 -> d,
+  p=0.5 -> sqrt(d), p=-1 -> 1/d; otherwise ``np.power``.
+* ``x.std(axis=1)`` = sqrt(pairwise((x - pairwise(x)/k)**2) / k).
+
+Parity is pinned by the golden vectors in ``tests/golden/`` that were produced
+by importing the reference ``interpolator.py`` itself
+(``tests/golden/make_golden.py``).
+"""
+from __future__ import annotations
+
+import math
+import os
+from concurrent.futures import ProcessPoolExecutor
+
+import numpy as np
+
+EPS = 1e-10  # interpolator.py:102 and :142
+
+
+# ----------------------------------------------------------------------------
+# numpy's reduction order, restated (used by the GPU epilogue contract)
+# ----------------------------------------------------------------------------
+def pairwise_sum(a) -> float:
+    """numpy ``@TYPE@_pairwise_sum`` for a contiguous 1-D float64 run.
+
+    n < 8: sequential from 0.0; 8 <= n <= 128: eight strided accumulators,
+    ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the n%8 tail sequentially;
+    n > 128: split at n/2 rounded down to a multiple of 8 and recurse.
+    The reduction result is ``0.0 + pairwise_sum(row)`` (identity first).
+    """
+    n = len(a)
+    if n < 8:
+        res = 0.0
+        for v in a:
+            res += float(v)
+        return res
+    if n <= 128:
+        r = [float(a[j]) for j in range(8)]
+        i = 8
+        stop = n - (n % 8)
+        while i < stop:
+            for j in range(8):
+                r[j] += float(a[i + j])
+            i += 8
+        res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]))
+        while i < n:
+            res += float(a[i])
+            i += 1
+        return res
+    n2 = n // 2
+    n2 -= n2 % 8
+    return pairwise_sum(a[:n2]) + pairwise_sum(a[n2:])
+
+
+def numpy_power(d: np.ndarray, p: float) -> np.ndarray:
+    """``d ** p`` exactly as ndarray.__pow__ evaluates it (scalar fast paths)."""
+    if p == 2.0:
+        return d * d
+    if p == 1.0:
+        return d.copy()
+    if p == 0.5:
+        return np.sqrt(d)
+    if p == -1.0:
+        with np.errstate(divide="ignore"):
+            return 1.0 / d
+    return np.power(d, p)
+
+
+# ----------------------------------------------------------------------------
+# k-NN
+# ----------------------------------------------------------------------------
+def knn_kdtree(points: np.ndarray, queries: np.ndarray, k: int):
+    """scipy KDTree query, as interpolator.py:132 (build) and :139 (query)."""
+    from scipy.spatial import KDTree
+
+    tree = KDTree(points)
+    return tree.query(queries, k=k)
+
+
+def knn_bruteforce(points: np.ndarray, queries: np.ndarray, k: int, chunk: int = 2048):
+    """Exact brute-force k-NN (small cases only): ties broken by lower index.
+
+    Distances use the cKDTree p=2 order ``(dx*dx + dy*dy) + dz*dz`` then sqrt.
+    """
+    points = np.ascontiguousarray(points, dtype=np.float64)
+    queries = np.ascontiguousarray(queries, dtype=np.float64)
+    nq = queries.shape[0]
+    dist = np.empty((nq, k))
+    idx = np.empty((nq, k), dtype=np.int64)
+    for s in range(0, nq, chunk):
+        q = queries[s : s + chunk]
+        dx = q[:, None, 0] - points[None, :, 0]
+        dy = q[:, None, 1] - points[None, :, 1]
+        dz = q[:, None, 2] - points[None, :, 2]
+        d2 = (dx * dx + dy * dy) + dz * dz
+        order = np.argsort(d2, axis=1, kind="stable")[:, :k]
+        idx[s : s + chunk] = order
+        dist[s : s + chunk] = np.sqrt(np.take_along_axis(d2, order, axis=1))
+    return dist, idx
+
+
+# ----------------------------------------------------------------------------
+# weights + gather-sum (the per-voxel epilogue)
+# ----------------------------------------------------------------------------
+def idw_weights(dist: np.ndarray, power: float, eps: float = EPS) -> np.ndarray:
+    """interpolator.py:142-147 — w = 1/(d**p + eps), normalised by its row sum."""
+    w = 1.0 / (numpy_power(dist, power) + eps)
+    return w / w.sum(axis=1, keepdims=True)
+
+
+def sibson_weights(dist: np.ndarray, eps: float = EPS) -> np.ndarray:
+    """interpolator.py:102-116 — inverse-distance weights damped by exp(-d/std(d))."""
+    inv = 1.0 / (dist + eps)
+    w = inv / inv.sum(axis=1, keepdims=True)
+    sigma = dist.std(axis=1, keepdims=True)
+    with np.errstate(invalid="ignore", over="ignore", under="ignore"):
+        w = w * np.exp(-dist / (sigma + eps))
+        return w / w.sum(axis=1, keepdims=True)
+
+
+def gather_sum(weights: np.ndarray, values: np.ndarray, idx: np.ndarray) -> np.ndarray:
+    """interpolator.py:150-153 (and :119-122): per component sum_k w * values[idx]."""
+    out = np.zeros((weights.shape[0], 3))
+    for c in range(3):
+        out[:, c] = (weights * values[idx, c]).sum(axis=1)
+    return out
+
+
+def interp_points(points, values, queries, method="idw", k=8, power=2.0, knn="kdtree"):
+    """Interpolate at an (M,3) query list; returns (M,3) float64 (AoS like the reference)."""
+    points = np.asarray(points, dtype=np.float64)
+    values = np.asarray(values, dtype=np.float64)
+    queries = np.asarray(queries, dtype=np.float64).reshape(-1, 3)
+    if knn == "kdtree":
+        dist, idx = knn_kdtree(points, queries, k)
+    else:
+        dist, idx = knn_bruteforce(points, queries, k)
+    if method == "idw":
+        w = idw_weights(dist, power)
+    elif method == "sibson":
+        w = sibson_weights(dist)
+    else:
+        raise ValueError(method)
+    with np.errstate(invalid="ignore"):
+        return gather_sum(w, values, idx)
+
+
+def grid_queries(ax, ay, az, z0=0, z1=None):
+    """Voxel coordinates of the C-order (nz, ny, nx) grid, x fastest (interpolator.py:59,135)."""
+    z1 = len(az) if z1 is None else z1
+    Z, Y, X = np.meshgrid(np.asarray(az)[z0:z1], ay, ax, indexing="ij")
+    return np.stack([X.ravel(), Y.ravel(), Z.ravel()], axis=-1)
+
+
+def interp_grid(points, values, ax, ay, az, method="idw", k=8, power=2.0, z0=0, z1=None, knn="kdtree"):
+    """Whole-grid (or z-slab) interpolation -> (U, V, W) each (nz', ny, nx)."""
+    z1 = len(az) if z1 is None else z1
+    q = grid_queries(ax, ay, az, z0, z1)
+    out = interp_points(points, values, q, method, k, power, knn)
+    shape = (z1 - z0, len(ay), len(ax))
+    return tuple(np.ascontiguousarray(out[:, c].reshape(shape)) for c in range(3))
+
+
+# ----------------------------------------------------------------------------
+# multiprocess z-slab driver (interpolator.py:173-182 pattern) — CPU baseline
+# ----------------------------------------------------------------------------
+_W = {}
+
+
+def _worker_init(points, values, ax, ay, az, method, k, power):
+    _W.update(points=points, values=values, ax=ax, ay=ay, az=az, method=method, k=k, power=power)
+
+
+def _worker_slab(z_range):
+    z0, z1 = z_range
+    w = _W
+    return z0, interp_grid(w["points"], w["values"], w["ax"], w["ay"], w["az"], w["method"], w["k"], w["power"], z0, z1)
+
+
+def interp_grid_parallel(points, values, ax, ay, az, method="idw", k=8, power=2.0,
+                         z0=0, z1=None, n_jobs=None, slab=None):
+    """Fan z-slabs over a ProcessPoolExecutor, each worker holding its own KDTree.
+
+    Z-slab results are bit-identical to the whole-grid call for IDW/Sibson
+    (each voxel depends only on its coordinate and the full particle set).
+    """
+    z1 = len(az) if z1 is None else z1
+    n_jobs = n_jobs or os.cpu_count() or 1
+    planes = z1 - z0
+    slab = slab or max(1, math.ceil(planes / (4 * n_jobs)))
+    ranges = [(s, min(s + slab, z1)) for s in range(z0, z1, slab)]
+    shape = (planes, len(ay), len(ax))
+    U, V, W = (np.empty(shape) for _ in range(3))
+    with ProcessPoolExecutor(max_workers=n_jobs, initializer=_worker_init,
+                             initargs=(points, values, ax, ay, az, method, k, power)) as ex:
+        for s, (u, v, w) in ex.map(_worker_slab, ranges):
+            U[s - z0 : s - z0 + u.shape[0]] = u
+            V[s - z0 : s - z0 + u.shape[0]] = v
+            W[s - z0 : s - z0 + u.shape[0]] = w
+    return U, V, W
+
+
+def nan_fill_and_mask(U, V, W, fluid_mask=None):
+    """main.py:195-207 caller epilogue: nan_to_num if U has a NaN, zero solid voxels."""
+    if np.isnan(U).any():
+        U, V, W = np.nan_to_num(U), np.nan_to_num(V), np.nan_to_num(W)
+    if fluid_mask is not None:
+        solid = ~fluid_mask
+        U, V, W = U.copy(), V.copy(), W.copy()
+        U[solid] = 0
+        V[solid] = 0
+        W[solid] = 0
+    return U, V, W

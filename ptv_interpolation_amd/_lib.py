@@ -1,0 +1,217 @@
+"""ctypes binding of the C ABI in include/ptv_api.h (libptv_amd.so, built in-tree).
+
+The shipped path has no CPU fallback: if the library is missing or no GPU is
+visible, ``lib()`` / ``Context`` raise.  Structures mirror the header field by
+field.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("PTV_LIB", os.path.join(HERE, "libptv_amd.so"))
+
+PTV_OK = 0
+PTV_E_ARG = -1
+PTV_E_HIP = -2
+PTV_E_NOMEM = -3
+PTV_E_UNSUPPORTED = -4
+PTV_E_INEXACT = -5
+PTV_E_SINGULAR = -6
+
+METHOD_IDW = 0
+METHOD_SIBSON = 1
+METHOD_NEAREST = 2
+
+FLAG_NAN_TO_NUM = 1
+
+_dp = C.POINTER(C.c_double)
+
+
+class Particles(C.Structure):
+    _fields_ = [("n", C.c_int64), ("x", _dp), ("y", _dp), ("z", _dp), ("u", _dp), ("v", _dp), ("w", _dp)]
+
+
+class Grid(C.Structure):
+    _fields_ = [("nx", C.c_int64), ("ny", C.c_int64), ("nz", C.c_int64),
+                ("ax", _dp), ("ay", _dp), ("az", _dp),
+                ("px", _dp), ("py", _dp), ("pz", _dp),
+                ("z_begin", C.c_int64), ("z_end", C.c_int64)]
+
+
+class KnnParams(C.Structure):
+    _fields_ = [("method", C.c_int), ("k", C.c_int), ("power", C.c_double), ("eps", C.c_double),
+                ("fluid_mask", C.POINTER(C.c_uint8)), ("flags", C.c_uint32), ("cell_occupancy", C.c_double)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("ms_h2d", C.c_double), ("ms_bin", C.c_double), ("ms_knn", C.c_double), ("ms_d2h", C.c_double),
+                ("ms_total", C.c_double), ("n_particles", C.c_int64), ("n_voxels", C.c_int64),
+                ("n_cells", C.c_int64), ("cells", C.c_int32 * 3), ("levels", C.c_int32),
+                ("cell_size", C.c_double * 3)]
+
+    def as_dict(self):
+        d = {f: getattr(self, f) for f, _ in self._fields_}
+        d["cells"] = list(self.cells)
+        d["cell_size"] = list(self.cell_size)
+        return d
+
+
+EXPORTS = {
+    "ptv_version": (C.c_int, []),
+    "ptv_last_error": (C.c_char_p, []),
+    "ptv_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "ptv_init": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    "ptv_free": (C.c_int, [C.c_void_p]),
+    "ptv_interp_knn": (C.c_int, [C.c_void_p, C.POINTER(Particles), C.POINTER(Grid), C.POINTER(KnnParams),
+                                 _dp, _dp, _dp, C.POINTER(Stats)]),
+    "ptv_interp_knn_dev": (C.c_int, [C.c_void_p, C.POINTER(Particles), C.POINTER(Grid), C.POINTER(KnnParams),
+                                     _dp, _dp, _dp, C.c_void_p, C.POINTER(Stats)]),
+    "ptv_last_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class PtvError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"ptv error {code}: {msg}")
+        self.code = code
+        self.msg = msg
+
+
+def lib():
+    """Load libptv_amd.so (raises if it is missing: there is no CPU fallback)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise ImportError(
+                    f"{LIB_PATH} not found: build it with `python -m ptv_interpolation_amd.build` "
+                    "(hipcc, gfx950). The k-NN path has no CPU fallback.")
+            L = C.CDLL(LIB_PATH)
+            for name, (res, args) in EXPORTS.items():
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != PTV_OK:
+        msg = lib().ptv_last_error().decode(errors="replace")
+        if rc == PTV_E_ARG:
+            raise ValueError(msg)
+        if rc == PTV_E_NOMEM:
+            raise MemoryError(msg)
+        if rc == PTV_E_UNSUPPORTED:
+            raise NotImplementedError(msg)
+        raise PtvError(rc, msg)
+    return rc
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    check(lib().ptv_device_count(C.byref(n)))
+    return n.value
+
+
+def as_dp(a: np.ndarray):
+    return a.ctypes.data_as(_dp)
+
+
+def dev_dp(ptr: int):
+    return C.cast(C.c_void_p(ptr), _dp)
+
+
+class Context:
+    """One device context (stream + reusable device buffers)."""
+
+    _cache = {}
+
+    def __init__(self, device: int = 0):
+        L = lib()
+        h = C.c_void_p()
+        check(L.ptv_init(int(device), C.byref(h)))
+        self.h = h
+        self.device = int(device)
+
+    @classmethod
+    def get(cls, device: int = 0) -> "Context":
+        with _lock:
+            ctx = cls._cache.get(device)
+        if ctx is None:
+            ctx = cls(device)
+            with _lock:
+                cls._cache[device] = ctx
+        return ctx
+
+    def close(self):
+        if self.h:
+            lib().ptv_free(self.h)
+            self.h = None
+
+    def last_stats(self) -> dict:
+        st = Stats()
+        check(lib().ptv_last_stats(self.h, C.byref(st)))
+        return st.as_dict()
+
+    # -- host buffers ------------------------------------------------------
+    def interp_knn(self, points, values, axes=None, grid_points=None, shape=None, method=METHOD_IDW, k=8,
+                   power=2.0, eps=1e-10, fluid_mask=None, flags=0, z_range=None, cell_occupancy=0.0):
+        """Host-array k-NN interpolation. Returns (U, V, W) float64 (nz', ny, nx)."""
+        pts = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 3)
+        vals = np.ascontiguousarray(values, dtype=np.float64).reshape(-1, 3)
+        cols = [np.ascontiguousarray(pts[:, i]) for i in range(3)] + [np.ascontiguousarray(vals[:, i]) for i in range(3)]
+        P = Particles(pts.shape[0], *[as_dp(c) for c in cols])
+        keep = list(cols)
+        if axes is not None:
+            ax, ay, az = (np.ascontiguousarray(a, dtype=np.float64).ravel() for a in axes)
+            nx, ny, nz = len(ax), len(ay), len(az)
+            keep += [ax, ay, az]
+            G = Grid(nx, ny, nz, as_dp(ax), as_dp(ay), as_dp(az), None, None, None, 0, nz)
+        else:
+            nz, ny, nx = shape
+            gp = [np.ascontiguousarray(a, dtype=np.float64).ravel() for a in grid_points]
+            keep += gp
+            G = Grid(nx, ny, nz, None, None, None, as_dp(gp[0]), as_dp(gp[1]), as_dp(gp[2]), 0, nz)
+        z0, z1 = (0, nz) if z_range is None else z_range
+        G.z_begin, G.z_end = z0, z1
+        mk = None
+        if fluid_mask is not None:
+            mk = np.ascontiguousarray(fluid_mask, dtype=np.uint8).reshape(nz, ny, nx)
+            keep.append(mk)
+        prm = KnnParams(method, int(k), float(power), float(eps),
+                        mk.ctypes.data_as(C.POINTER(C.c_uint8)) if mk is not None else None, flags,
+                        float(cell_occupancy))
+        out = [np.empty((z1 - z0, ny, nx), dtype=np.float64) for _ in range(3)]
+        st = Stats()
+        check(lib().ptv_interp_knn(self.h, C.byref(P), C.byref(G), C.byref(prm),
+                                   as_dp(out[0]), as_dp(out[1]), as_dp(out[2]), C.byref(st)))
+        self.stats = st.as_dict()
+        return tuple(out)
+
+    # -- device buffers (integer device pointers, e.g. torch tensor data_ptr()) --
+    def interp_knn_dev(self, n, pptrs, nx, ny, nz, axes_ptrs=None, point_ptrs=None, out_ptrs=None,
+                       method=METHOD_IDW, k=8, power=2.0, eps=1e-10, mask_ptr=0, flags=0, z_range=None,
+                       stream=0, cell_occupancy=0.0):
+        P = Particles(int(n), *[dev_dp(p) for p in pptrs])
+        if axes_ptrs is not None:
+            G = Grid(nx, ny, nz, *[dev_dp(p) for p in axes_ptrs], None, None, None, 0, nz)
+        else:
+            G = Grid(nx, ny, nz, None, None, None, *[dev_dp(p) for p in point_ptrs], 0, nz)
+        z0, z1 = (0, nz) if z_range is None else z_range
+        G.z_begin, G.z_end = z0, z1
+        prm = KnnParams(method, int(k), float(power), float(eps),
+                        C.cast(C.c_void_p(mask_ptr), C.POINTER(C.c_uint8)) if mask_ptr else None, flags,
+                        float(cell_occupancy))
+        st = Stats()
+        check(lib().ptv_interp_knn_dev(self.h, C.byref(P), C.byref(G), C.byref(prm),
+                                       *[dev_dp(p) for p in out_ptrs], C.c_void_p(stream or 0), C.byref(st)))
+        return st.as_dict()

@@ -1,0 +1,74 @@
+"""Build the HIP C-ABI library ``libptv_amd.so`` in-tree for gfx950.
+
+Plain ``hipcc`` (no torch extension machinery): each translation unit is
+compiled to an object with ``--offload-arch=gfx950`` and linked into one
+shared library next to this file, so the snapshot that travels to the GPU
+box carries it.  ``-ffp-contract=off`` is load-bearing: the k-NN epilogue
+reproduces numpy's rounding sequence (no fused multiply-adds).
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+INCLUDE = os.path.join(os.path.dirname(HERE), "include")
+LIB = os.path.join(HERE, "libptv_amd.so")
+BUILD = os.path.join(HERE, "csrc", "_build")
+SOURCES = ["ptv_api.cpp", "ptv_bin.hip", "ptv_knn.hip"]
+ARCH = os.environ.get("PTV_OFFLOAD_ARCH", "gfx950")
+
+COMMON = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", f"--offload-arch={ARCH}",
+          "-I", INCLUDE, "-I", CSRC, "-Wno-unused-result"]
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (ROCm toolchain required to build libptv_amd.so)")
+
+
+def _stale(obj: str, deps) -> bool:
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(verbose: bool = False, force: bool = False) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    cc = hipcc()
+    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h"))]
+    headers.append(os.path.join(INCLUDE, "ptv_api.h"))
+    jobs = []
+    objs = []
+    for src in SOURCES:
+        sp = os.path.join(CSRC, src)
+        obj = os.path.join(BUILD, src + ".o")
+        objs.append(obj)
+        if force or _stale(obj, [sp, __file__] + headers):
+            lang = ["-x", "hip"] if src.endswith(".hip") else ["-x", "hip"]
+            jobs.append([cc, *COMMON, *lang, "-c", sp, "-o", obj])
+
+    def run(cmd):
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        return r
+
+    with ThreadPoolExecutor(max_workers=min(4, max(1, len(jobs)))) as ex:
+        list(ex.map(run, jobs))
+    if force or jobs or _stale(LIB, objs):
+        run([cc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", LIB])
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(verbose=True, force="--force" in sys.argv))

@@ -1,0 +1,457 @@
+// ptv_api.cpp — C ABI (include/ptv_api.h): context, device buffers, host/device entry points.
+//
+// The Python drop-in (ptv_interpolation_amd/interpolator.py) binds these symbols with
+// ctypes; nothing here depends on torch.  One context = one device + one stream +
+// grow-only device buffers reused across calls (the reference rebuilds its KDTree on
+// every call, interpolator.py:90/:132; here the binning runs every call too, but no
+// allocation does once the buffers are warm).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+
+#include "../../include/ptv_api.h"
+#include "ptv_kernels.hpp"
+
+namespace ptv {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string &msg) { g_last_error = msg; }
+
+template <typename T>
+struct DevBuf {
+    T *p = nullptr;
+    size_t cap = 0;  // elements
+    int ensure(size_t n) {
+        if (n <= cap && p) return PTV_OK;
+        if (p) hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(n, 1);
+        hipError_t e = hipMalloc(&p, want * sizeof(T));
+        if (e != hipSuccess) {
+            p = nullptr;
+            set_error("hipMalloc of " + std::to_string(want * sizeof(T)) + " bytes failed: " + hipGetErrorString(e));
+            return PTV_E_NOMEM;
+        }
+        cap = want;
+        return PTV_OK;
+    }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+}  // namespace ptv
+
+using namespace ptv;
+
+struct ptv_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev_knn0 = nullptr, ev_knn1 = nullptr, ev_bin0 = nullptr, ev_bin1 = nullptr;
+    bool timed_pending = false;
+    DevBuf<double> pin[6], axes, qpts[3], out[3];
+    DevBuf<uint8_t> mask;
+    DevBuf<uint32_t> code, perm, count, start, scanp;
+    DevBuf<double4> prec, pval;
+    DevBuf<double> bbox_part, bbox_out;
+    double *h_bbox = nullptr;  // pinned, 6 doubles
+    ptv_stats last{};
+};
+
+#define PTV_TRY(expr)               \
+    do {                            \
+        int _r = (expr);            \
+        if (_r != PTV_OK) return _r; \
+    } while (0)
+
+extern "C" {
+
+int ptv_version(void) { return PTV_API_VERSION; }
+
+const char *ptv_last_error(void) { return g_last_error.c_str(); }
+
+int ptv_device_count(int *out) {
+    if (!out) {
+        set_error("ptv_device_count: out is NULL");
+        return PTV_E_ARG;
+    }
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    *out = n;
+    return PTV_OK;
+}
+
+int ptv_init(int device, ptv_ctx **out) {
+    if (!out) {
+        set_error("ptv_init: out is NULL");
+        return PTV_E_ARG;
+    }
+    *out = nullptr;
+    int n = 0;
+    PTV_HIP(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) {
+        set_error("ptv_init: device " + std::to_string(device) + " out of range (" + std::to_string(n) + " visible)");
+        return PTV_E_ARG;
+    }
+    PTV_HIP(hipSetDevice(device));
+    ptv_ctx *c = new ptv_ctx();
+    c->device = device;
+    PTV_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    PTV_HIP(hipEventCreate(&c->ev_knn0));
+    PTV_HIP(hipEventCreate(&c->ev_knn1));
+    PTV_HIP(hipEventCreate(&c->ev_bin0));
+    PTV_HIP(hipEventCreate(&c->ev_bin1));
+    PTV_HIP(hipHostMalloc(&c->h_bbox, 8 * sizeof(double)));
+    *out = c;
+    return PTV_OK;
+}
+
+int ptv_free(ptv_ctx *c) {
+    if (!c) return PTV_OK;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    for (auto &b : c->pin) b.release();
+    for (auto &b : c->qpts) b.release();
+    for (auto &b : c->out) b.release();
+    c->axes.release();
+    c->mask.release();
+    c->code.release();
+    c->perm.release();
+    c->count.release();
+    c->start.release();
+    c->scanp.release();
+    c->prec.release();
+    c->pval.release();
+    c->bbox_part.release();
+    c->bbox_out.release();
+    if (c->h_bbox) hipHostFree(c->h_bbox);
+    hipEventDestroy(c->ev_knn0);
+    hipEventDestroy(c->ev_knn1);
+    hipEventDestroy(c->ev_bin0);
+    hipEventDestroy(c->ev_bin1);
+    hipStreamDestroy(c->stream);
+    delete c;
+    return PTV_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+int validate(const ptv_particles *p, const ptv_grid *g, const ptv_knn_params *prm) {
+    if (!p || !g || !prm) {
+        set_error("NULL particles/grid/params");
+        return PTV_E_ARG;
+    }
+    if (p->n <= 0 || !p->x || !p->y || !p->z || !p->u || !p->v || !p->w) {
+        set_error("particles: need n > 0 and six non-NULL arrays");
+        return PTV_E_ARG;
+    }
+    if (p->n >= (int64_t)1 << 31) {
+        set_error("particles: n must be < 2^31");
+        return PTV_E_ARG;
+    }
+    if (g->nx <= 0 || g->ny <= 0 || g->nz <= 0 || g->nx > (1 << 30) || g->ny > (1 << 30)) {
+        set_error("grid: dimensions must be positive");
+        return PTV_E_ARG;
+    }
+    const bool sep = g->ax && g->ay && g->az;
+    const bool pts = g->px && g->py && g->pz;
+    if (!sep && !pts) {
+        set_error("grid: give either the three axes or the three point arrays");
+        return PTV_E_ARG;
+    }
+    if (g->z_begin < 0 || g->z_end > g->nz || g->z_begin > g->z_end) {
+        set_error("grid: bad z slab [" + std::to_string(g->z_begin) + ", " + std::to_string(g->z_end) + ")");
+        return PTV_E_ARG;
+    }
+    if (prm->method != PTV_METHOD_IDW && prm->method != PTV_METHOD_SIBSON && prm->method != PTV_METHOD_NEAREST) {
+        set_error("unknown method " + std::to_string(prm->method));
+        return PTV_E_ARG;
+    }
+    if (prm->k < 1) {
+        set_error("k must be >= 1");
+        return PTV_E_ARG;
+    }
+    if ((int64_t)prm->k > p->n) {
+        set_error("k=" + std::to_string(prm->k) + " exceeds the number of particles " + std::to_string(p->n));
+        return PTV_E_ARG;
+    }
+    if (kmax_for(prm->k) == 0) {
+        set_error("k=" + std::to_string(prm->k) + " exceeds the GPU k-NN list limit (64)");
+        return PTV_E_UNSUPPORTED;
+    }
+    return PTV_OK;
+}
+
+// Cell grid over the union bounding box: ~`occ` particles per cell on average.
+CellGrid make_cell_grid(const double lo_in[3], const double hi_in[3], int64_t n, double occ) {
+    CellGrid cg{};
+    double ext[3], lo[3];
+    double maxext = 0.0, maxabs = 0.0;
+    for (int a = 0; a < 3; ++a) {
+        lo[a] = lo_in[a];
+        ext[a] = hi_in[a] - lo_in[a];
+        if (!(ext[a] > 0.0)) ext[a] = 0.0;
+        maxext = std::max(maxext, ext[a]);
+        maxabs = std::max(maxabs, std::max(std::fabs(lo_in[a]), std::fabs(hi_in[a])));
+    }
+    if (!(occ > 0.0)) occ = 3.0;
+    double vol = 1.0;
+    int dims = 0;
+    for (int a = 0; a < 3; ++a)
+        if (ext[a] > 1e-9 * maxext) {
+            vol *= ext[a];
+            ++dims;
+        }
+    double cs = dims ? std::pow(occ * vol / (double)n, 1.0 / dims) : 1.0;
+    int maxnc = 1;
+    for (int a = 0; a < 3; ++a) {
+        int nc = 1;
+        if (ext[a] > 1e-9 * maxext && cs > 0.0) {
+            double f = std::ceil(ext[a] / cs);
+            nc = (int)std::min(512.0, std::max(1.0, f));
+        }
+        cg.nc[a] = nc;
+        maxnc = std::max(maxnc, nc);
+        cg.cs[a] = ext[a] > 0.0 ? ext[a] / nc : 1.0;
+        cg.ic[a] = 1.0 / cg.cs[a];
+        cg.o[a] = lo[a];
+        cg.mg[a] = 1e-12 * (maxabs + maxext) + 1e-12 * cg.cs[a];
+    }
+    int L = 0;
+    while ((1 << L) < maxnc) ++L;
+    cg.L = L;
+    return cg;
+}
+
+int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn_params *prm, const double *ax,
+            const double *ay, const double *az, const double *qx, const double *qy, const double *qz,
+            const uint8_t *mask, double *U, double *V, double *W, hipStream_t s, ptv_stats *st) {
+    const int64_t n = p->n;
+    const bool sep = ax != nullptr;
+    const int64_t plane = g->nx * g->ny;
+    const int64_t z0 = g->z_begin, z1 = g->z_end;
+    const int64_t nvox = (z1 - z0) * plane;
+
+    // 1. bounding box of particles + this slab's queries
+    PTV_TRY(c->bbox_part.ensure(6 * 1024));
+    PTV_TRY(c->bbox_out.ensure(8));
+    const double *pp[3] = {p->x, p->y, p->z};
+    const double *qa[3];
+    int64_t qn[3];
+    if (sep) {
+        qa[0] = ax;
+        qa[1] = ay;
+        qa[2] = az + z0;
+        qn[0] = g->nx;
+        qn[1] = g->ny;
+        qn[2] = z1 - z0;
+    } else {
+        qa[0] = qx + z0 * plane;
+        qa[1] = qy + z0 * plane;
+        qa[2] = qz + z0 * plane;
+        qn[0] = qn[1] = qn[2] = nvox;
+    }
+    PTV_HIP(hipEventRecord(c->ev_bin0, s));
+    PTV_TRY(launch_bbox(pp, n, qa, qn, c->bbox_part.p, 1024, c->bbox_out.p, s));
+    PTV_HIP(hipMemcpyAsync(c->h_bbox, c->bbox_out.p, 6 * sizeof(double), hipMemcpyDeviceToHost, s));
+    PTV_HIP(hipStreamSynchronize(s));
+    double lo[3] = {c->h_bbox[0], c->h_bbox[1], c->h_bbox[2]};
+    double hi[3] = {c->h_bbox[3], c->h_bbox[4], c->h_bbox[5]};
+    for (int a = 0; a < 3; ++a) {
+        if (!std::isfinite(lo[a]) || !std::isfinite(hi[a])) {
+            set_error("non-finite particle or grid coordinates");
+            return PTV_E_ARG;
+        }
+    }
+
+    // 2. binning
+    CellGrid cg = make_cell_grid(lo, hi, n, prm->cell_occupancy);
+    const size_t P = (size_t)1 << cg.L;
+    const size_t m = P * P * P;
+    PTV_TRY(c->code.ensure(n));
+    PTV_TRY(c->perm.ensure(n));
+    PTV_TRY(c->prec.ensure(n));
+    PTV_TRY(c->pval.ensure(n));
+    PTV_TRY(c->count.ensure(m));
+    PTV_TRY(c->start.ensure(m + 1));
+    PTV_TRY(c->scanp.ensure(scan_partials_needed(m) + 1));
+    const double *pv[3] = {p->u, p->v, p->w};
+    PTV_TRY(launch_bin(cg, pp, pv, n, c->code.p, c->perm.p, c->count.p, c->start.p, c->scanp.p, c->prec.p,
+                       c->pval.p, s));
+    PTV_HIP(hipEventRecord(c->ev_bin1, s));
+
+    // 3. k-NN interpolation
+    KnnLaunch kl;
+    kl.cg = cg;
+    kl.nx = (int)g->nx;
+    kl.ny = (int)g->ny;
+    kl.nz = (int)g->nz;
+    kl.z0 = (int)z0;
+    kl.z1 = (int)z1;
+    kl.separable = sep ? 1 : 0;
+    kl.method = prm->method == PTV_METHOD_NEAREST ? PTV_METHOD_IDW : prm->method;
+    kl.k = prm->k;
+    kl.power = prm->power;
+    kl.eps = prm->eps;
+    kl.flags = prm->flags;
+    Binned b{c->prec.p, c->pval.p, c->start.p, n};
+    PTV_HIP(hipEventRecord(c->ev_knn0, s));
+    PTV_TRY(launch_knn(kl, b, ax, ay, az, qx, qy, qz, mask, U, V, W, s));
+    PTV_HIP(hipEventRecord(c->ev_knn1, s));
+    c->timed_pending = true;
+
+    ptv_stats &ls = c->last;
+    ls = ptv_stats{};
+    ls.n_particles = n;
+    ls.n_voxels = nvox;
+    ls.n_cells = (int64_t)cg.nc[0] * cg.nc[1] * cg.nc[2];
+    for (int a = 0; a < 3; ++a) {
+        ls.cells[a] = cg.nc[a];
+        ls.cell_size[a] = cg.cs[a];
+    }
+    ls.levels = cg.L;
+    if (st) *st = ls;
+    return PTV_OK;
+}
+
+int finish_timing(ptv_ctx *c) {
+    if (!c->timed_pending) return PTV_OK;
+    PTV_HIP(hipEventSynchronize(c->ev_knn1));
+    float ms = 0.f;
+    PTV_HIP(hipEventElapsedTime(&ms, c->ev_knn0, c->ev_knn1));
+    c->last.ms_knn = ms;
+    PTV_HIP(hipEventElapsedTime(&ms, c->ev_bin0, c->ev_bin1));
+    c->last.ms_bin = ms;
+    c->timed_pending = false;
+    return PTV_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ptv_interp_knn_dev(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn_params *prm, double *U,
+                       double *V, double *W, void *stream, ptv_stats *st) {
+    if (!c) {
+        set_error("NULL context");
+        return PTV_E_ARG;
+    }
+    PTV_TRY(validate(p, g, prm));
+    if (!U || !V || !W) {
+        set_error("NULL output");
+        return PTV_E_ARG;
+    }
+    PTV_HIP(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    const bool sep = g->ax && g->ay && g->az;
+    return run_knn(c, p, g, prm, sep ? g->ax : nullptr, sep ? g->ay : nullptr, sep ? g->az : nullptr,
+                   sep ? nullptr : g->px, sep ? nullptr : g->py, sep ? nullptr : g->pz, prm->fluid_mask, U, V, W, s,
+                   st);
+}
+
+int ptv_interp_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn_params *prm, double *U,
+                   double *V, double *W, ptv_stats *st) {
+    if (!c) {
+        set_error("NULL context");
+        return PTV_E_ARG;
+    }
+    PTV_TRY(validate(p, g, prm));
+    if (!U || !V || !W) {
+        set_error("NULL output");
+        return PTV_E_ARG;
+    }
+    PTV_HIP(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    hipEvent_t t0, t1, t2;
+    PTV_HIP(hipEventCreate(&t0));
+    PTV_HIP(hipEventCreate(&t1));
+    PTV_HIP(hipEventCreate(&t2));
+    PTV_HIP(hipEventRecord(t0, s));
+    const int64_t n = p->n;
+    const int64_t plane = g->nx * g->ny;
+    const int64_t nvox = (g->z_end - g->z_begin) * plane;
+    const int64_t nfull = g->nz * plane;
+    // H2D: particles
+    const double *src[6] = {p->x, p->y, p->z, p->u, p->v, p->w};
+    for (int i = 0; i < 6; ++i) {
+        PTV_TRY(c->pin[i].ensure(n));
+        PTV_HIP(hipMemcpyAsync(c->pin[i].p, src[i], n * sizeof(double), hipMemcpyHostToDevice, s));
+    }
+    ptv_particles dp{n, c->pin[0].p, c->pin[1].p, c->pin[2].p, c->pin[3].p, c->pin[4].p, c->pin[5].p};
+    ptv_grid dg = *g;
+    const bool sep = g->ax && g->ay && g->az;
+    if (sep) {
+        PTV_TRY(c->axes.ensure(g->nx + g->ny + g->nz));
+        PTV_HIP(hipMemcpyAsync(c->axes.p, g->ax, g->nx * sizeof(double), hipMemcpyHostToDevice, s));
+        PTV_HIP(hipMemcpyAsync(c->axes.p + g->nx, g->ay, g->ny * sizeof(double), hipMemcpyHostToDevice, s));
+        PTV_HIP(hipMemcpyAsync(c->axes.p + g->nx + g->ny, g->az, g->nz * sizeof(double), hipMemcpyHostToDevice, s));
+        dg.ax = c->axes.p;
+        dg.ay = c->axes.p + g->nx;
+        dg.az = c->axes.p + g->nx + g->ny;
+        dg.px = dg.py = dg.pz = nullptr;
+    } else {
+        const double *q[3] = {g->px, g->py, g->pz};
+        for (int i = 0; i < 3; ++i) {
+            PTV_TRY(c->qpts[i].ensure(nfull));
+            PTV_HIP(hipMemcpyAsync(c->qpts[i].p, q[i], nfull * sizeof(double), hipMemcpyHostToDevice, s));
+        }
+        dg.ax = dg.ay = dg.az = nullptr;
+        dg.px = c->qpts[0].p;
+        dg.py = c->qpts[1].p;
+        dg.pz = c->qpts[2].p;
+    }
+    const uint8_t *dmask = nullptr;
+    if (prm->fluid_mask) {
+        PTV_TRY(c->mask.ensure(nfull));
+        PTV_HIP(hipMemcpyAsync(c->mask.p, prm->fluid_mask, nfull, hipMemcpyHostToDevice, s));
+        dmask = c->mask.p;
+    }
+    for (int i = 0; i < 3; ++i) PTV_TRY(c->out[i].ensure(nvox));
+    PTV_HIP(hipEventRecord(t1, s));
+    PTV_TRY(run_knn(c, &dp, &dg, prm, dg.ax, dg.ay, dg.az, dg.px, dg.py, dg.pz, dmask, c->out[0].p, c->out[1].p,
+                    c->out[2].p, s, nullptr));
+    PTV_HIP(hipEventRecord(t2, s));
+    double *dst[3] = {U, V, W};
+    for (int i = 0; i < 3; ++i)
+        PTV_HIP(hipMemcpyAsync(dst[i], c->out[i].p, nvox * sizeof(double), hipMemcpyDeviceToHost, s));
+    hipEvent_t t3;
+    PTV_HIP(hipEventCreate(&t3));
+    PTV_HIP(hipEventRecord(t3, s));
+    PTV_HIP(hipStreamSynchronize(s));
+    PTV_TRY(finish_timing(c));
+    float h2d = 0.f, d2h = 0.f, tot = 0.f;
+    PTV_HIP(hipEventElapsedTime(&h2d, t0, t1));
+    PTV_HIP(hipEventElapsedTime(&d2h, t2, t3));
+    PTV_HIP(hipEventElapsedTime(&tot, t0, t3));
+    c->last.ms_h2d = h2d;
+    c->last.ms_d2h = d2h;
+    c->last.ms_total = tot;
+    hipEventDestroy(t0);
+    hipEventDestroy(t1);
+    hipEventDestroy(t2);
+    hipEventDestroy(t3);
+    if (st) *st = c->last;
+    return PTV_OK;
+}
+
+int ptv_last_stats(ptv_ctx *c, ptv_stats *st) {
+    if (!c || !st) {
+        set_error("NULL argument");
+        return PTV_E_ARG;
+    }
+    PTV_HIP(hipSetDevice(c->device));
+    PTV_TRY(finish_timing(c));
+    *st = c->last;
+    return PTV_OK;
+}
+
+}  // extern "C"

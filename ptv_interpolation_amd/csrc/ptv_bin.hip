@@ -1,0 +1,323 @@
+// ptv_bin.hip — spatial-hash particle binning for the k-NN interpolator (gfx950).
+//
+// Replaces the role of the per-call cKDTree build in the reference
+// (interpolator.py:90 and :132, scipy KDTree(points), leafsize 10): particles
+// are counting-sorted into a uniform cell grid addressed by Morton code on a
+// padded 2^L cube, so that every octree node is a contiguous particle range.
+//
+//   bbox        per-axis min/max of particles and queries (grid-stride, LDS reduce)
+//   cell_code   Morton code per particle + atomic histogram
+//   scan        exclusive prefix sum of the P^3 histogram (3-phase, 4096 cells/block)
+//   scatter     particle -> slot (atomic fill from the back of each cell)
+//   seg_sort    ascending original index inside each cell (deterministic order)
+//   gather      AoS records for the scalar-load k-NN kernel:
+//                 prec[slot] = (x, y, z, id), pval[slot] = (u, v, w, 0)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+
+#include "../../include/ptv_api.h"
+#include "ptv_kernels.hpp"
+
+namespace ptv {
+
+// ---------------------------------------------------------------------------
+// bounding box
+// ---------------------------------------------------------------------------
+struct BBoxArgs {
+    const double *p[3];
+    const double *q[3];
+    int64_t n;
+    int64_t qn[3];
+};
+
+__global__ __launch_bounds__(256) void k_bbox(BBoxArgs a, double *partials) {
+    double lo[3], hi[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        lo[d] = INFINITY;
+        hi[d] = -INFINITY;
+    }
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (int64_t i = t0; i < a.n; i += stride) {
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            double v = a.p[d][i];
+            lo[d] = fmin(lo[d], v);
+            hi[d] = fmax(hi[d], v);
+        }
+    }
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        for (int64_t i = t0; i < a.qn[d]; i += stride) {
+            double v = a.q[d][i];
+            lo[d] = fmin(lo[d], v);
+            hi[d] = fmax(hi[d], v);
+        }
+    }
+    __shared__ double red[6][256];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        red[d][threadIdx.x] = lo[d];
+        red[3 + d][threadIdx.x] = hi[d];
+    }
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) {
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                red[d][threadIdx.x] = fmin(red[d][threadIdx.x], red[d][threadIdx.x + s]);
+                red[3 + d][threadIdx.x] = fmax(red[3 + d][threadIdx.x], red[3 + d][threadIdx.x + s]);
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < 6) partials[(size_t)blockIdx.x * 6 + threadIdx.x] = red[threadIdx.x][0];
+}
+
+__global__ __launch_bounds__(64) void k_bbox_final(const double *partials, int nblk, double *out) {
+    const int d = threadIdx.x;
+    if (d >= 6) return;
+    double r = d < 3 ? INFINITY : -INFINITY;
+    for (int b = 0; b < nblk; ++b) {
+        double v = partials[(size_t)b * 6 + d];
+        r = d < 3 ? fmin(r, v) : fmax(r, v);
+    }
+    out[d] = r;
+}
+
+int launch_bbox(const double *const px[3], int64_t n, const double *const qa[3], const int64_t qn[3],
+                double *d_partials, int max_blocks, double *d_out6, hipStream_t s) {
+    BBoxArgs a;
+    int64_t m = n;
+    for (int d = 0; d < 3; ++d) {
+        a.p[d] = px[d];
+        a.q[d] = qa[d];
+        a.qn[d] = qn[d];
+        m = std::max(m, qn[d]);
+    }
+    a.n = n;
+    int nblk = (int)std::min<int64_t>((m + 255) / 256, max_blocks);
+    nblk = std::max(nblk, 1);
+    hipLaunchKernelGGL(k_bbox, dim3(nblk), dim3(256), 0, s, a, d_partials);
+    hipLaunchKernelGGL(k_bbox_final, dim3(1), dim3(64), 0, s, (const double *)d_partials, nblk, d_out6);
+    PTV_HIP(hipGetLastError());
+    return PTV_OK;
+}
+
+// ---------------------------------------------------------------------------
+// cell codes + histogram
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int cell_coord(double v, double o, double ic, int nc) {
+    double f = floor((v - o) * ic);
+    int c = (f < 0.0) ? 0 : (f >= (double)nc ? nc - 1 : (int)f);
+    return c;
+}
+
+__global__ __launch_bounds__(256) void k_cell_code(CellGrid cg, const double *__restrict__ x,
+                                                   const double *__restrict__ y, const double *__restrict__ z,
+                                                   int64_t n, uint32_t *__restrict__ code,
+                                                   uint32_t *__restrict__ count) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int cx = cell_coord(x[i], cg.o[0], cg.ic[0], cg.nc[0]);
+    int cy = cell_coord(y[i], cg.o[1], cg.ic[1], cg.nc[1]);
+    int cz = cell_coord(z[i], cg.o[2], cg.ic[2], cg.nc[2]);
+    uint32_t c = morton3((uint32_t)cx, (uint32_t)cy, (uint32_t)cz);
+    code[i] = c;
+    atomicAdd(&count[c], 1u);
+}
+
+// ---------------------------------------------------------------------------
+// exclusive scan of m uint32 counts -> start[0..m] (start[m] = total)
+// ---------------------------------------------------------------------------
+constexpr int kScanThreads = 256;
+constexpr int kScanItems = 16;
+constexpr int kScanTile = kScanThreads * kScanItems;  // 4096
+
+size_t scan_partials_needed(size_t m) { return (m + kScanTile - 1) / kScanTile + 1; }
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_scan_reduce(const uint32_t *__restrict__ in, size_t m,
+                                                              uint32_t *__restrict__ partials) {
+    size_t base = (size_t)blockIdx.x * kScanTile + (size_t)threadIdx.x * kScanItems;
+    uint32_t s = 0;
+#pragma unroll
+    for (int j = 0; j < kScanItems; ++j) {
+        size_t i = base + j;
+        s += (i < m) ? in[i] : 0u;
+    }
+    // block reduce
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    __shared__ uint32_t ws[kScanThreads / 64];
+    if (lane == 0) ws[wid] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < kScanThreads / 64; ++w) t += ws[w];
+        partials[blockIdx.x] = t;
+    }
+}
+
+// single-block exclusive scan of the block partials (in place), total -> partials[nb]
+__global__ __launch_bounds__(1024) void k_scan_partials(uint32_t *partials, int nb) {
+    __shared__ uint32_t ws[16];
+    __shared__ uint32_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int base = 0; base < nb; base += 1024) {
+        int i = base + threadIdx.x;
+        uint32_t v = (i < nb) ? partials[i] : 0u;
+        uint32_t inc = wave_incl_scan(v);
+        if (lane == 63) ws[wid] = inc;
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            uint32_t t = (threadIdx.x < 16) ? ws[threadIdx.x] : 0u;
+            uint32_t ti = wave_incl_scan(t);
+            if (threadIdx.x < 16) ws[threadIdx.x] = ti - t;
+        }
+        __syncthreads();
+        uint32_t excl = carry + ws[wid] + inc - v;
+        __syncthreads();
+        if (i < nb) partials[i] = excl;
+        if (threadIdx.x == 1023) carry = excl + v;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partials[nb] = carry;
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_scan_final(const uint32_t *__restrict__ in, size_t m,
+                                                             const uint32_t *__restrict__ partials, int nb,
+                                                             uint32_t *__restrict__ out) {
+    size_t base = (size_t)blockIdx.x * kScanTile + (size_t)threadIdx.x * kScanItems;
+    uint32_t v[kScanItems];
+    uint32_t s = 0;
+#pragma unroll
+    for (int j = 0; j < kScanItems; ++j) {
+        size_t i = base + j;
+        v[j] = (i < m) ? in[i] : 0u;
+        s += v[j];
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t inc = wave_incl_scan(s);
+    __shared__ uint32_t ws[kScanThreads / 64];
+    if (lane == 63) ws[wid] = inc;
+    __syncthreads();
+    uint32_t off = partials[blockIdx.x];
+    for (int w = 0; w < wid; ++w) off += ws[w];
+    uint32_t run = off + inc - s;
+#pragma unroll
+    for (int j = 0; j < kScanItems; ++j) {
+        size_t i = base + j;
+        if (i < m) out[i] = run;
+        run += v[j];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) out[m] = partials[nb];
+}
+
+// ---------------------------------------------------------------------------
+// scatter + deterministic in-cell order
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_scatter(const uint32_t *__restrict__ code, int64_t n,
+                                                 const uint32_t *__restrict__ start, uint32_t *__restrict__ fill,
+                                                 uint32_t *__restrict__ perm) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t c = code[i];
+    uint32_t slot = start[c] + atomicSub(&fill[c], 1u) - 1u;
+    perm[slot] = (uint32_t)i;
+}
+
+__device__ void sift_down(uint32_t *a, int root, int n) {
+    while (true) {
+        int child = 2 * root + 1;
+        if (child >= n) return;
+        if (child + 1 < n && a[child + 1] > a[child]) child++;
+        if (a[root] >= a[child]) return;
+        uint32_t t = a[root];
+        a[root] = a[child];
+        a[child] = t;
+        root = child;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_seg_sort(const uint32_t *__restrict__ start, size_t m,
+                                                  uint32_t *__restrict__ perm) {
+    size_t c = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= m) return;
+    uint32_t s = start[c], e = start[c + 1];
+    int n = (int)(e - s);
+    if (n <= 1) return;
+    uint32_t *a = perm + s;
+    if (n <= 48) {
+        for (int i = 1; i < n; ++i) {
+            uint32_t v = a[i];
+            int j = i - 1;
+            while (j >= 0 && a[j] > v) {
+                a[j + 1] = a[j];
+                --j;
+            }
+            a[j + 1] = v;
+        }
+    } else {  // pathological clustering: heap sort, O(n log n), still deterministic
+        for (int r = n / 2 - 1; r >= 0; --r) sift_down(a, r, n);
+        for (int end = n - 1; end > 0; --end) {
+            uint32_t t = a[0];
+            a[0] = a[end];
+            a[end] = t;
+            sift_down(a, 0, end);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_gather(const uint32_t *__restrict__ perm, int64_t n,
+                                                const double *__restrict__ x, const double *__restrict__ y,
+                                                const double *__restrict__ z, const double *__restrict__ u,
+                                                const double *__restrict__ v, const double *__restrict__ w,
+                                                double4 *__restrict__ prec, double4 *__restrict__ pval) {
+    int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    uint32_t i = perm[s];
+    prec[s] = make_double4(x[i], y[i], z[i], (double)i);
+    pval[s] = make_double4(u[i], v[i], w[i], 0.0);
+}
+
+int launch_bin(const CellGrid &cg, const double *const px[3], const double *const pv[3], int64_t n,
+               uint32_t *d_code, uint32_t *d_perm, uint32_t *d_count, uint32_t *d_start,
+               uint32_t *d_scan_partials, double4 *d_prec, double4 *d_pval, hipStream_t s) {
+    const size_t P = (size_t)1 << cg.L;
+    const size_t m = P * P * P;
+    PTV_HIP(hipMemsetAsync(d_count, 0, m * sizeof(uint32_t), s));
+    const int nb = (int)((n + 255) / 256);
+    hipLaunchKernelGGL(k_cell_code, dim3(nb), dim3(256), 0, s, cg, px[0], px[1], px[2], n, d_code, d_count);
+    const int sb = (int)((m + kScanTile - 1) / kScanTile);
+    hipLaunchKernelGGL(k_scan_reduce, dim3(sb), dim3(kScanThreads), 0, s, (const uint32_t *)d_count, m,
+                       d_scan_partials);
+    hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(1024), 0, s, d_scan_partials, sb);
+    hipLaunchKernelGGL(k_scan_final, dim3(sb), dim3(kScanThreads), 0, s, (const uint32_t *)d_count, m,
+                       (const uint32_t *)d_scan_partials, sb, d_start);
+    hipLaunchKernelGGL(k_scatter, dim3(nb), dim3(256), 0, s, (const uint32_t *)d_code, n,
+                       (const uint32_t *)d_start, d_count, d_perm);
+    hipLaunchKernelGGL(k_seg_sort, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, (const uint32_t *)d_start, m,
+                       d_perm);
+    hipLaunchKernelGGL(k_gather, dim3(nb), dim3(256), 0, s, (const uint32_t *)d_perm, n, px[0], px[1], px[2],
+                       pv[0], pv[1], pv[2], d_prec, d_pval);
+    PTV_HIP(hipGetLastError());
+    return PTV_OK;
+}
+
+}  // namespace ptv

@@ -1,0 +1,41 @@
+// ptv_kernels.hpp — host-side launchers for the device kernels.
+#pragma once
+
+#include "ptv_common.hpp"
+
+namespace ptv {
+
+// ---- binning (ptv_bin.hip) ----
+// Per-axis min/max over the particles and the query coordinates.
+// Query coordinates: separable axes (qa[a] has qn[a] entries) or point lists.
+int launch_bbox(const double *const px[3], int64_t n, const double *const qa[3], const int64_t qn[3],
+                double *d_partials, int max_blocks, double *d_out6, hipStream_t s);
+
+// Counting-sort the particles into Morton-ordered cells (deterministic order
+// inside each cell: ascending original index).  Scratch buffers must hold
+// n entries (code, perm) and P^3 (+1) entries (count, start).
+int launch_bin(const CellGrid &cg, const double *const px[3], const double *const pv[3], int64_t n,
+               uint32_t *d_code, uint32_t *d_perm, uint32_t *d_count, uint32_t *d_start,
+               uint32_t *d_scan_partials, double4 *d_prec, double4 *d_pval, hipStream_t s);
+
+size_t scan_partials_needed(size_t m);
+
+// ---- k-NN interpolation (ptv_knn.hip) ----
+struct KnnLaunch {
+    CellGrid cg;
+    int nx, ny, nz;      // full grid
+    int z0, z1;          // planes computed by this launch
+    int separable;       // 1: axes, 0: point lists
+    int method;          // PTV_METHOD_*
+    int k;
+    double power, eps;
+    uint32_t flags;
+};
+
+int kmax_for(int k);  // compile-time list length serving k, 0 if unsupported
+
+int launch_knn(const KnnLaunch &a, const Binned &b, const double *ax, const double *ay, const double *az,
+               const double *qx, const double *qy, const double *qz, const uint8_t *mask, double *U, double *V,
+               double *W, hipStream_t s);
+
+}  // namespace ptv

@@ -1,0 +1,215 @@
+"""Drop-in replacement for the reference ``interpolator`` module (MI355X path).
+
+Same public names and signatures as tombultreys/ptv_interpolation
+``interpolator.py`` so ``main.py``, ``test_parallel.py`` and the dataset run
+scripts import it unchanged (put this repo first on ``PYTHONPATH``; the repo
+root ``interpolator.py`` re-exports this module):
+
+    load_ptv_data        interpolator.py:9-26
+    load_mask            interpolator.py:28-39
+    create_grid          interpolator.py:41-60
+    interpolate_field    interpolator.py:65-203   <- idw / sibson run on the GPU
+    sample_mask_on_grid  interpolator.py:205-238
+    extract_boundary_particles  interpolator.py:240-284
+
+``interpolate_field(method='idw'|'sibson')`` runs the k-NN search and the
+weighted average as HIP kernels through the C ABI (include/ptv_api.h).  There is
+no CPU fallback for these methods: a missing library or GPU raises.  Results
+reproduce the reference arithmetic (see ptv_interpolation_amd/csrc/ptv_knn.hip);
+``n_jobs`` is accepted and ignored by the GPU methods (the reference uses it only
+for RBF, interpolator.py:173).  ``linear``/``nearest``/``cubic`` are scipy
+``griddata`` calls in the reference (interpolator.py:196-197) and stay so here
+(outside the accelerated path).
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+from . import _lib
+
+__all__ = [
+    "load_ptv_data",
+    "load_mask",
+    "create_grid",
+    "interpolate_field",
+    "sample_mask_on_grid",
+    "extract_boundary_particles",
+]
+
+_EPS = 1e-10  # interpolator.py:102, :142
+
+
+# ---------------------------------------------------------------------------
+# I/O and grid helpers (host side, same behaviour as the reference)
+# ---------------------------------------------------------------------------
+def load_ptv_data(filepath):
+    """CSV -> DataFrame with columns x, y, z, u, v, w (vx/vy/vz renamed); interpolator.py:9-26."""
+    import pandas as pd
+
+    try:
+        df = pd.read_csv(filepath)
+        df.rename(columns={"vx": "u", "vy": "v", "vz": "w"}, inplace=True)
+        need = {"x", "y", "z", "u", "v", "w"}
+        if not need.issubset(df.columns):
+            raise ValueError(f"CSV must contain columns: {need}")
+        return df
+    except Exception as e:  # the reference wraps every failure as IOError
+        raise IOError(f"Error reading {filepath}: {e}")
+
+
+def load_mask(filepath):
+    """3-D TIFF -> bool (True = fluid, i.e. > 0); interpolator.py:28-39."""
+    try:
+        import tifffile
+
+        return tifffile.imread(filepath) > 0
+    except Exception as e:
+        raise IOError(f"Error reading mask {filepath}: {e}")
+
+
+def create_grid(bounds, resolution, dense=True):
+    """Regular grid: axes ``linspace(min, max-1, n)``; (X, Y, Z) of shape (nz, ny, nx).
+
+    interpolator.py:41-60.  ``dense=False`` returns read-only zero-stride
+    broadcast views with identical shape and values (no 3*8*V-byte meshgrids);
+    ``interpolate_field`` recognises either form as a separable grid.
+    """
+    (xmin, xmax), (ymin, ymax), (zmin, zmax) = bounds
+    if isinstance(resolution, int):
+        nx = ny = nz = resolution
+    else:
+        nx, ny, nz = resolution
+    x = np.linspace(xmin, xmax - 1, nx)
+    y = np.linspace(ymin, ymax - 1, ny)
+    z = np.linspace(zmin, zmax - 1, nz)
+    if dense:
+        Z, Y, X = np.meshgrid(z, y, x, indexing="ij")
+    else:
+        shape = (nz, ny, nx)
+        X = np.broadcast_to(x[None, None, :], shape)
+        Y = np.broadcast_to(y[None, :, None], shape)
+        Z = np.broadcast_to(z[:, None, None], shape)
+    return (X, Y, Z), (x, y, z)
+
+
+def sample_mask_on_grid(mask_raw, grid_tuple, bounds_raw):
+    """Nearest-neighbour resampling of a raw mask onto the grid; interpolator.py:205-238."""
+    from scipy.interpolate import RegularGridInterpolator
+
+    nz, ny, nx = mask_raw.shape
+    (xmin, xmax), (ymin, ymax), (zmin, zmax) = bounds_raw
+    X, Y, Z = grid_tuple
+    axes = []
+    for lo, hi, n in ((zmin, zmax, nz), (ymin, ymax, ny), (xmin, xmax, nx)):
+        axes.append(np.linspace(lo, hi - 1, n) if n > 1 else np.array([lo]))
+    rgi = RegularGridInterpolator(tuple(axes), mask_raw.astype(float), method="nearest",
+                                  bounds_error=False, fill_value=0)
+    pts = np.stack([np.ravel(Z), np.ravel(Y), np.ravel(X)], axis=-1)
+    return rgi(pts).reshape(X.shape) > 0.5
+
+
+def extract_boundary_particles(mask, bounds, sampling_step=1, thickness=1):
+    """Solid voxels within `thickness` 6-connected steps of fluid -> coordinates; interpolator.py:240-284."""
+    import scipy.ndimage
+
+    if mask is None:
+        return np.array([]), np.array([]), np.array([])
+    nz, ny, nx = mask.shape
+    (xmin, xmax), (ymin, ymax), (zmin, zmax) = bounds
+    st = scipy.ndimage.generate_binary_structure(3, 1)
+    grown = scipy.ndimage.binary_dilation(mask, structure=st, iterations=thickness)
+    iz, iy, ix = np.where(grown & ~mask)
+    if len(ix) == 0:
+        return np.array([]), np.array([]), np.array([])
+    if sampling_step > 1:
+        iz, iy, ix = iz[::sampling_step], iy[::sampling_step], ix[::sampling_step]
+
+    def phys(idx, lo, hi, n):
+        return lo + idx * (hi - 1 - lo) / (n - 1) if n > 1 else np.full_like(idx, lo)
+
+    return phys(ix, xmin, xmax, nx), phys(iy, ymin, ymax, ny), phys(iz, zmin, zmax, nz)
+
+
+# ---------------------------------------------------------------------------
+# grid introspection
+# ---------------------------------------------------------------------------
+def separable_axes(X, Y, Z):
+    """Return (ax, ay, az) if (X, Y, Z) is an (nz, ny, nx) meshgrid(z, y, x, 'ij'), else None."""
+    X, Y, Z = np.asarray(X), np.asarray(Y), np.asarray(Z)
+    if X.ndim != 3 or X.shape != Y.shape or X.shape != Z.shape or X.size == 0:
+        return None
+    ax = np.ascontiguousarray(X[0, 0, :], dtype=np.float64)
+    ay = np.ascontiguousarray(Y[0, :, 0], dtype=np.float64)
+    az = np.ascontiguousarray(Z[:, 0, 0], dtype=np.float64)
+
+    def fits(A, ref):
+        if A.strides.count(0) == 2:  # zero-stride broadcast view (create_grid(dense=False))
+            return True
+        return np.array_equal(A, np.broadcast_to(ref, A.shape))
+
+    if fits(X, ax[None, None, :]) and fits(Y, ay[None, :, None]) and fits(Z, az[:, None, None]):
+        return ax, ay, az
+    return None
+
+
+def _gpu_device():
+    return int(os.environ.get("PTV_DEVICE", "0"))
+
+
+def _knn_field(points, values, grid_tuple, method, k, power):
+    """GPU k-NN IDW/Sibson over the caller's grid; returns (U, V, W) with X's shape."""
+    X, Y, Z = grid_tuple
+    shape = np.shape(X)
+    n = points.shape[0]
+    if k < 1:
+        raise ValueError(f"k must be a positive integer, got {k}")
+    if n == 0:
+        raise ValueError("no particles to interpolate from")
+    if k == 1:
+        # the reference's KDTree.query(k=1) squeezes to (V,), then .sum(axis=1) fails
+        raise np.exceptions.AxisError("axis 1 is out of bounds for array of dimension 1")
+    if k > n:
+        # KDTree pads missing neighbours with index n; values[indices] then fails
+        raise IndexError(f"index {n} is out of bounds for axis 0 with size {n}")
+    ctx = _lib.Context.get(_gpu_device())
+    m = _lib.METHOD_IDW if method == "idw" else _lib.METHOD_SIBSON
+    axes = separable_axes(X, Y, Z)
+    if axes is not None:
+        U, V, W = ctx.interp_knn(points, values, axes=axes, method=m, k=k, power=power, eps=_EPS)
+    else:
+        size = int(np.prod(shape))
+        g = [np.ascontiguousarray(np.asarray(A, dtype=np.float64)).reshape(-1) for A in (X, Y, Z)]
+        sh = tuple(shape) if len(shape) == 3 else (1, 1, size)
+        U, V, W = ctx.interp_knn(points, values, grid_points=g, shape=sh, method=m, k=k, power=power, eps=_EPS)
+    return U.reshape(shape), V.reshape(shape), W.reshape(shape)
+
+
+def interpolate_field(df, grid_tuple, method="linear", rbf_neighbors=20, rbf_kernel="thin_plate_spline",
+                      smoothing=0.0, n_jobs=1, idw_power=2.0, idw_neighbors=50, sibson_neighbors=30):
+    """Interpolate PTV particles onto the grid (interpolator.py:65-203 signature and semantics).
+
+    Returns ``(U, V, W)`` float64 arrays of the grid's shape.
+    """
+    X, Y, Z = grid_tuple
+    points = np.asarray(df[["x", "y", "z"]].values, dtype=np.float64)
+    values = np.asarray(df[["u", "v", "w"]].values, dtype=np.float64)
+
+    if method == "sibson":
+        print(f"Using Sibson (Natural Neighbor) Interpolation (neighbors={sibson_neighbors})...")
+        return _knn_field(points, values, grid_tuple, "sibson", int(sibson_neighbors), 2.0)
+    if method == "idw":
+        print(f"Using IDW Interpolation (power={idw_power}, neighbors={idw_neighbors})...")
+        return _knn_field(points, values, grid_tuple, "idw", int(idw_neighbors), float(idw_power))
+    if method == "rbf":
+        print(f"Using RBF Interpolation ({rbf_kernel}) with {rbf_neighbors} neighbors, "
+              f"smoothing={smoothing} and n_jobs={n_jobs}...")
+        from . import rbf as _rbf
+
+        return _rbf.rbf_field(points, values, grid_tuple, int(rbf_neighbors), rbf_kernel, float(smoothing))
+    # scattered-data griddata methods: not part of the accelerated path (interpolator.py:196-197)
+    from scipy.interpolate import griddata
+
+    out = griddata(points, values, (X, Y, Z), method=method, fill_value=0.0)
+    return out[..., 0], out[..., 1], out[..., 2]

@@ -1,0 +1,202 @@
+"""Generate the golden parity fixtures by importing the reference interpolator.
+
+Runs only where the read-only reference checkout exists (default
+``/root/reference``); the GPU box never runs it, it only reads the committed
+``*.npz`` files.  ``tifffile`` is not installed in this image and is only used
+by the reference's TIFF I/O (interpolator.py:35, main.py:230), so a stub module
+is placed in ``sys.modules`` before the import.
+
+Every fixture stores its inputs (particles, values, 1-D grid axes, parameters)
+and the reference outputs ``U, V, W`` (C-order (nz, ny, nx) float64), plus the
+numpy/scipy versions they were produced with.  Particle coordinates are
+continuous random draws so that no two particles tie at the k-th distance
+(cKDTree's tie order is traversal dependent) except in the
+explicitly-tied edge cases, which are checked normwise only.
+
+Usage:  python tests/golden/make_golden.py [--ref /root/reference]
+"""
+from __future__ import annotations
+
+import argparse
+import contextlib
+import io
+import os
+import sys
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _import_reference(path):
+    sys.modules.setdefault("tifffile", types.ModuleType("tifffile"))
+    sys.path.insert(0, path)
+    import interpolator  # noqa: E402  (the reference module)
+
+    return interpolator
+
+
+def _df(points, values):
+    import pandas as pd
+
+    return pd.DataFrame({"x": points[:, 0], "y": points[:, 1], "z": points[:, 2],
+                         "u": values[:, 0], "v": values[:, 1], "w": values[:, 2]})
+
+
+def _save(name, **arrays):
+    import scipy
+
+    arrays.setdefault("numpy_version", np.array(np.__version__))
+    arrays.setdefault("scipy_version", np.array(scipy.__version__))
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrays)
+    print("wrote", name)
+
+
+def _run(ref, points, values, bounds, res, **kw):
+    (X, Y, Z), (x, y, z) = ref.create_grid(bounds, res)
+    with contextlib.redirect_stdout(io.StringIO()):
+        U, V, W = ref.interpolate_field(_df(points, values), (X, Y, Z), **kw)
+    return x, y, z, np.ascontiguousarray(U), np.ascontiguousarray(V), np.ascontiguousarray(W)
+
+
+def knn_cases(ref):
+    rng = np.random.default_rng(20260213)
+
+    # (1) headline-shaped IDW: k=8, p=2, unit-spaced 32^3 grid, 5k particles
+    P = rng.uniform(-0.5, 31.5, (5000, 3)); Q = rng.standard_normal((5000, 3))
+    x, y, z, U, V, W = _run(ref, P, Q, ((0, 32),) * 3, 32, method="idw", idw_neighbors=8, idw_power=2.0)
+    _save("idw_k8_p2", points=P, values=Q, ax=x, ay=y, az=z, method=np.array("idw"), k=8, power=2.0, U=U, V=V, W=W)
+
+    # (2) IDW k=50, p=1.5 (pow path)
+    P = rng.uniform(0, 23, (4000, 3)); Q = rng.standard_normal((4000, 3))
+    x, y, z, U, V, W = _run(ref, P, Q, ((0, 24),) * 3, 24, method="idw", idw_neighbors=50, idw_power=1.5)
+    _save("idw_k50_p1.5", points=P, values=Q, ax=x, ay=y, az=z, method=np.array("idw"), k=50, power=1.5, U=U, V=V, W=W)
+
+    # (3) reference defaults (idw_neighbors=50, idw_power=2.0; interpolator.py:65)
+    P = rng.uniform(0, 19, (3000, 3)); Q = rng.standard_normal((3000, 3))
+    x, y, z, U, V, W = _run(ref, P, Q, ((0, 20),) * 3, 20, method="idw")
+    _save("idw_default_k50", points=P, values=Q, ax=x, ay=y, az=z, method=np.array("idw"), k=50, power=2.0, U=U, V=V, W=W)
+
+    # (4) Sibson k=30
+    P = rng.uniform(0, 23, (4000, 3)); Q = rng.standard_normal((4000, 3))
+    x, y, z, U, V, W = _run(ref, P, Q, ((0, 24),) * 3, 24, method="sibson", sibson_neighbors=30)
+    _save("sibson_k30", points=P, values=Q, ax=x, ay=y, az=z, method=np.array("sibson"), k=30, power=2.0, U=U, V=V, W=W)
+
+    # (5) anisotropic grid in physical units, particles beyond the grid box, odd k
+    P = np.stack([rng.uniform(-4.0, 6.0, 3000), rng.uniform(9.0, 15.0, 3000), rng.uniform(0.0, 2.5, 3000)], 1)
+    Q = rng.standard_normal((3000, 3))
+    x, y, z, U, V, W = _run(ref, P, Q, ((-3.2, 5.1), (10.0, 14.0), (0.5, 2.0)), (20, 12, 9),
+                            method="idw", idw_neighbors=13, idw_power=2.0)
+    _save("idw_aniso_k13", points=P, values=Q, ax=x, ay=y, az=z, method=np.array("idw"), k=13, power=2.0, U=U, V=V, W=W)
+
+    # (6) Sibson on the same anisotropic set with the reference default k
+    x, y, z, U, V, W = _run(ref, P, Q, ((-3.2, 5.1), (10.0, 14.0), (0.5, 2.0)), (20, 12, 9), method="sibson")
+    _save("sibson_aniso_k30", points=P, values=Q, ax=x, ay=y, az=z, method=np.array("sibson"), k=30, power=2.0, U=U, V=V, W=W)
+
+    # (7) small k values and p = 1, 0.5, -1, 3 (numpy fast paths and pow)
+    P = rng.uniform(0, 11, (600, 3)); Q = rng.standard_normal((600, 3))
+    for k, p in ((2, 1.0), (5, 0.5), (7, -1.0), (9, 3.0), (16, 2.0), (33, 2.0), (64, 2.0)):
+        x, y, z, U, V, W = _run(ref, P, Q, ((0, 12),) * 3, 12, method="idw", idw_neighbors=k, idw_power=p)
+        _save(f"idw_small_k{k}_p{p}", points=P, values=Q, ax=x, ay=y, az=z, method=np.array("idw"), k=k, power=p, U=U, V=V, W=W)
+    for k in (2, 7, 8, 17, 64):
+        x, y, z, U, V, W = _run(ref, P, Q, ((0, 12),) * 3, 12, method="sibson", sibson_neighbors=k)
+        _save(f"sibson_small_k{k}", points=P, values=Q, ax=x, ay=y, az=z, method=np.array("sibson"), k=k, power=2.0, U=U, V=V, W=W)
+
+
+def edge_cases(ref):
+    rng = np.random.default_rng(7)
+    # voxel coincident with a particle: weight 1/(0 + 1e-10) dominates
+    P = rng.uniform(0, 9, (400, 3)); P[:40] = np.round(P[:40]); Q = rng.standard_normal((400, 3))
+    x, y, z, U, V, W = _run(ref, P, Q, ((0, 10),) * 3, 10, method="idw", idw_neighbors=8)
+    _save("edge_coincident_idw", points=P, values=Q, ax=x, ay=y, az=z, method=np.array("idw"), k=8, power=2.0, U=U, V=V, W=W, tied=1)
+    x, y, z, U, V, W = _run(ref, P, Q, ((0, 10),) * 3, 10, method="sibson", sibson_neighbors=8)
+    _save("edge_coincident_sibson", points=P, values=Q, ax=x, ay=y, az=z, method=np.array("sibson"), k=8, power=2.0, U=U, V=V, W=W, tied=1)
+    # k == N
+    P = rng.uniform(0, 7, (12, 3)); Q = rng.standard_normal((12, 3))
+    x, y, z, U, V, W = _run(ref, P, Q, ((0, 8),) * 3, 8, method="idw", idw_neighbors=12)
+    _save("edge_k_eq_n", points=P, values=Q, ax=x, ay=y, az=z, method=np.array("idw"), k=12, power=2.0, U=U, V=V, W=W)
+    # Sibson sigma = 0: the 8 corners of a cube around voxel (2,2,2) -> all distances equal -> NaN
+    c = np.array([[2 + sx, 2 + sy, 2 + sz] for sx in (-1, 1) for sy in (-1, 1) for sz in (-1, 1)], float)
+    P = np.concatenate([c, rng.uniform(6, 9, (20, 3))]); Q = rng.standard_normal((28, 3))
+    x, y, z, U, V, W = _run(ref, P, Q, ((0, 10),) * 3, 10, method="sibson", sibson_neighbors=8)
+    assert np.isnan(U[2, 2, 2])
+    _save("edge_sibson_sigma0", points=P, values=Q, ax=x, ay=y, az=z, method=np.array("sibson"), k=8, power=2.0, U=U, V=V, W=W, tied=1)
+
+
+def masked_case(ref):
+    """main.py:78-207 masked pipeline, reproduced with the reference functions."""
+    sys.path.insert(0, os.path.join(HERE, "..", ".."))
+    from ptv_interpolation_amd import synth
+
+    G = 48
+    fluid = synth.fluid_mask(G)                        # mask_raw (True = fluid), interpolator.py:37
+    pts, _ = synth.sphere_pack(6000, G, seed=11)
+    vals = np.random.default_rng(12).standard_normal((6000, 3))
+    bounds = ((0, G), (0, G), (0, G))                  # main.py:105-106
+    keep = (pts >= 0).all(1) & (pts < G).all(1)        # main.py:140-142
+    pts, vals = pts[keep], vals[keep]
+    res = (32, 32, 32)                                 # --downscale 1.5 -> round(48/1.5), main.py:115-119
+    (X, Y, Z), (x, y, z) = ref.create_grid(bounds, res)
+    mask = ref.sample_mask_on_grid(fluid, (X, Y, Z), bounds_raw=bounds)
+    bx, by, bz = ref.extract_boundary_particles(fluid, bounds, sampling_step=3, thickness=1)
+    P = np.concatenate([pts, np.stack([bx, by, bz], 1)])
+    Q = np.concatenate([vals, np.zeros((len(bx), 3))])
+    with contextlib.redirect_stdout(io.StringIO()):
+        U, V, W = ref.interpolate_field(_df(P, Q), (X, Y, Z), method="idw", idw_neighbors=8)
+    Ur, Vr, Wr = (np.ascontiguousarray(a) for a in (U, V, W))
+    if np.isnan(U).any():                               # main.py:195-199
+        U, V, W = np.nan_to_num(U), np.nan_to_num(V), np.nan_to_num(W)
+    U, V, W = U.copy(), V.copy(), W.copy()
+    U[~mask] = 0; V[~mask] = 0; W[~mask] = 0            # main.py:202-207
+    _save("masked_spherepack_idw", points=P, values=Q, ax=x, ay=y, az=z, method=np.array("idw"), k=8, power=2.0,
+          mask=mask, fluid_raw=fluid, U_raw=Ur, V_raw=Vr, W_raw=Wr, U=U, V=V, W=W, tied=1)
+
+
+def rbf_cases(ref):
+    """Local RBF fixtures (interpolator.py:157-195 and scipy RBFInterpolator directly)."""
+    from scipy.interpolate import RBFInterpolator
+
+    rng = np.random.default_rng(99)
+    P = rng.uniform(0, 11, (1500, 3)); Q = rng.standard_normal((1500, 3))
+    for kern, k, s in (("thin_plate_spline", 20, 0.0), ("thin_plate_spline", 32, 5.0), ("cubic", 20, 0.0),
+                       ("quintic", 24, 0.0), ("linear", 16, 0.0)):
+        x, y, z, U, V, W = _run(ref, P, Q, ((0, 12),) * 3, 12, method="rbf", rbf_neighbors=k, rbf_kernel=kern, smoothing=s)
+        _save(f"rbf_{kern}_k{k}_s{s}", points=P, values=Q, ax=x, ay=y, az=z, method=np.array("rbf"),
+              kernel=np.array(kern), k=k, smoothing=s, U=U, V=V, W=W)
+    # Gaussian is not reachable through interpolate_field (no epsilon pass-through, interpolator.py:162-167):
+    # scipy oracle only, degree 0 (33x33 at k=32) and degree -1 (32x32).
+    (X, Y, Z), (x, y, z) = ref.create_grid(((0, 12),) * 3, 12)
+    flat = np.stack([X.ravel(), Y.ravel(), Z.ravel()], -1)
+    for deg in (0, -1):
+        out = RBFInterpolator(P, Q, neighbors=32, kernel="gaussian", epsilon=0.3, degree=deg)(flat)
+        U, V, W = (np.ascontiguousarray(out[:, c].reshape(X.shape)) for c in range(3))
+        _save(f"rbf_gaussian_eps0.3_k32_deg{deg}", points=P, values=Q, ax=x, ay=y, az=z, method=np.array("rbf"),
+              kernel=np.array("gaussian"), k=32, smoothing=0.0, epsilon=0.3, degree=deg, U=U, V=V, W=W)
+    # test_parallel.py:6-28 input (5 particles, neighbors clamps to N)
+    P5 = np.array([[0, 0, 0], [10, 0, 0], [0, 10, 0], [10, 10, 0], [5, 5, 5]], float)
+    Q5 = np.array([[1, 0, 0], [1, 0, 0], [1, 0, 0], [1, 0, 0], [2, 0, 0]], float)
+    x, y, z, U, V, W = _run(ref, P5, Q5, ((0, 10),) * 3, 10, method="rbf", n_jobs=1)
+    _save("rbf_test_parallel", points=P5, values=Q5, ax=x, ay=y, az=z, method=np.array("rbf"),
+          kernel=np.array("thin_plate_spline"), k=20, smoothing=0.0, U=U, V=V, W=W)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--only", default="knn,edge,masked,rbf")
+    a = ap.parse_args()
+    ref = _import_reference(a.ref)
+    only = a.only.split(",")
+    if "knn" in only:
+        knn_cases(ref)
+    if "edge" in only:
+        edge_cases(ref)
+    if "masked" in only:
+        masked_case(ref)
+    if "rbf" in only:
+        rbf_cases(ref)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,154 @@
+"""GPU parity: the HIP k-NN path (through the C ABI) against the reference golden
+vectors and the oracle.  Runs only on an MI355X (``-m gpu``).
+
+Bar: IDW with numpy's exact power paths (p in {2, 1, 0.5, -1})
+must be bit-identical to the reference on tie-free inputs; pow/exp paths
+(p = 1.5, 3; Sibson) and tied inputs are checked normwise, max|d|/max|ref|
+<= 1e-10 per component (fp64).
+"""
+import numpy as np
+import pandas as pd
+import pytest
+
+from tests._util import load, names, normwise
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-10
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from ptv_interpolation_amd import _lib
+
+    if _lib.device_count() < 1:
+        pytest.fail("no GPU visible: the gpu tests must run on an MI355X")
+    return _lib.Context.get(0)
+
+
+def _exact(g):
+    return (not int(g.get("tied", 0))) and str(g["method"]) == "idw" and float(g["power"]) in (2.0, 1.0, 0.5, -1.0)
+
+
+def _method(g):
+    from ptv_interpolation_amd import _lib
+
+    return _lib.METHOD_IDW if str(g["method"]) == "idw" else _lib.METHOD_SIBSON
+
+
+@pytest.mark.parametrize("name", names(("idw", "sibson", "edge")))
+def test_golden_parity(ctx, name):
+    g = load(name)
+    U, V, W = ctx.interp_knn(g["points"], g["values"], axes=(g["ax"], g["ay"], g["az"]), method=_method(g),
+                             k=int(g["k"]), power=float(g["power"]))
+    for a, b in ((U, g["U"]), (V, g["V"]), (W, g["W"])):
+        assert normwise(a, b) <= TOL
+        if _exact(g):
+            assert np.array_equal(a, b, equal_nan=True), f"not bit-exact: {np.sum(a != b)} voxels differ"
+
+
+def test_masked_fused_epilogue(ctx):
+    """main.py:195-207 (NaN fill + solid zeroing) fused into the kernel."""
+    from ptv_interpolation_amd import _lib
+
+    g = load("masked_spherepack_idw")
+    axes = (g["ax"], g["ay"], g["az"])
+    Ur, Vr, Wr = ctx.interp_knn(g["points"], g["values"], axes=axes, k=8, power=2.0)
+    for a, b in ((Ur, g["U_raw"]), (Vr, g["V_raw"]), (Wr, g["W_raw"])):
+        assert normwise(a, b) <= TOL
+    U, V, W = ctx.interp_knn(g["points"], g["values"], axes=axes, k=8, power=2.0, fluid_mask=g["mask"],
+                             flags=_lib.FLAG_NAN_TO_NUM)
+    for a, b in ((U, g["U"]), (V, g["V"]), (W, g["W"])):
+        assert normwise(a, b) <= TOL
+    assert (U[~g["mask"]] == 0).all()
+
+
+def test_dropin_interpolate_field(golden_dir):
+    """The drop-in module reproduces the reference through its public signature."""
+    from ptv_interpolation_amd import interpolator as ip
+
+    g = load("idw_k8_p2")
+    df = pd.DataFrame({c: g["points"][:, i] for i, c in enumerate("xyz")} |
+                      {c: g["values"][:, i] for i, c in enumerate("uvw")})
+    (X, Y, Z), _ = ip.create_grid(((0, 32),) * 3, 32)
+    U, V, W = ip.interpolate_field(df, (X, Y, Z), method="idw", idw_neighbors=8, idw_power=2.0)
+    assert U.shape == (32, 32, 32) and U.dtype == np.float64
+    assert np.array_equal(U, g["U"]) and np.array_equal(V, g["V"]) and np.array_equal(W, g["W"])
+    # zero-stride grid views give the same answer
+    (Xb, Yb, Zb), _ = ip.create_grid(((0, 32),) * 3, 32, dense=False)
+    U2, _, _ = ip.interpolate_field(df, (Xb, Yb, Zb), method="idw", idw_neighbors=8)
+    assert np.array_equal(U2, U)
+
+
+def test_dropin_errors():
+    from ptv_interpolation_amd import interpolator as ip
+
+    g = load("edge_k_eq_n")
+    df = pd.DataFrame({c: g["points"][:, i] for i, c in enumerate("xyz")} |
+                      {c: g["values"][:, i] for i, c in enumerate("uvw")})
+    grid, _ = ip.create_grid(((0, 8),) * 3, 8)
+    with pytest.raises(np.exceptions.AxisError):
+        ip.interpolate_field(df, grid, method="idw", idw_neighbors=1)
+    with pytest.raises(IndexError):
+        ip.interpolate_field(df, grid, method="idw", idw_neighbors=13)
+    with pytest.raises(IndexError):
+        ip.interpolate_field(df, grid, method="sibson", sibson_neighbors=13)
+
+
+def test_point_list_mode(ctx):
+    """Non-separable query grid (a rotated lattice) goes through the point-list kernel path."""
+    from oracle import cpu_ref
+
+    rng = np.random.default_rng(5)
+    P = rng.uniform(-10, 10, (20000, 3)); Q = rng.standard_normal((20000, 3))
+    t = 0.3
+    i, j, l = np.meshgrid(np.arange(12), np.arange(10), np.arange(14), indexing="ij")
+    X = np.cos(t) * l - np.sin(t) * j - 6.0
+    Y = np.sin(t) * l + np.cos(t) * j - 5.0
+    Z = i - 6.0 + 0.1 * l
+    U, V, W = ctx.interp_knn(P, Q, grid_points=(X, Y, Z), shape=X.shape, k=8)
+    ref = cpu_ref.interp_points(P, Q, np.stack([X.ravel(), Y.ravel(), Z.ravel()], -1), "idw", 8, 2.0)
+    assert np.array_equal(U.ravel(), ref[:, 0]) and np.array_equal(W.ravel(), ref[:, 2])
+
+
+def test_slabs_equal_whole(ctx):
+    g = load("idw_k8_p2")
+    axes = (g["ax"], g["ay"], g["az"])
+    Uw, Vw, Ww = ctx.interp_knn(g["points"], g["values"], axes=axes, k=8)
+    parts = [ctx.interp_knn(g["points"], g["values"], axes=axes, k=8, z_range=(a, b))
+             for a, b in ((0, 5), (5, 13), (13, 32))]
+    assert np.array_equal(np.concatenate([p[0] for p in parts]), Uw)
+    assert np.array_equal(np.concatenate([p[2] for p in parts]), Ww)
+
+
+@pytest.mark.parametrize("k", [8, 50])
+def test_spherepack_voids_vs_oracle(ctx, k):
+    """Sphere-pack voids (empty sphere interiors) at 96^3 / 60k particles: exact vs KDTree."""
+    from oracle import cpu_ref
+    from ptv_interpolation_amd import synth
+
+    G = 96
+    P, Q = synth.sphere_pack(60000, G, values="normal")
+    ax = np.linspace(0, G - 1, G)
+    U, V, W = ctx.interp_knn(P, Q, axes=(ax, ax, ax), k=k)
+    Ur, Vr, Wr = cpu_ref.interp_grid(P, Q, ax, ax, ax, "idw", k, 2.0)
+    assert np.array_equal(U, Ur) and np.array_equal(V, Vr) and np.array_equal(W, Wr)
+
+
+@pytest.mark.parametrize("G,N,k", [(256, 1_000_000, 8), (512, 5_000_000, 8)])
+def test_full_size_sampled(ctx, G, N, k):
+    """Headline sizes: every voxel computed on the GPU, 20k random voxels checked bit-exact vs KDTree."""
+    from oracle import cpu_ref
+    from ptv_interpolation_amd import synth
+
+    P, Q = synth.sphere_pack(N, G, values="normal")
+    ax = np.linspace(0, G - 1, G)
+    U, V, W = ctx.interp_knn(P, Q, axes=(ax, ax, ax), k=k)
+    assert np.isfinite(U).all()
+    rng = np.random.default_rng(1)
+    idx = rng.integers(0, G, size=(20000, 3))
+    q = np.stack([ax[idx[:, 2]], ax[idx[:, 1]], ax[idx[:, 0]]], -1)
+    ref = cpu_ref.interp_points(P, Q, q, "idw", k, 2.0)
+    got = np.stack([U[idx[:, 0], idx[:, 1], idx[:, 2]], V[idx[:, 0], idx[:, 1], idx[:, 2]],
+                    W[idx[:, 0], idx[:, 1], idx[:, 2]]], -1)
+    assert np.array_equal(got, ref)

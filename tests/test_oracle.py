@@ -1,0 +1,63 @@
+"""The oracle (oracle/cpu_ref.py) pinned against the reference's own outputs.
+
+Golden vectors come from importing the reference interpolator.py
+(tests/golden/make_golden.py).  IDW/Sibson with p=2 are required bit-exact;
+pow/exp paths and tied inputs are normwise (<= 1e-10).
+"""
+import numpy as np
+import pytest
+
+from oracle import cpu_ref
+from tests._util import load, names, normwise
+
+
+def _bit_exact_expected(g):
+    return int(g.get("tied", 0)) == 0 and str(g["method"]) == "idw" and float(g["power"]) in (2.0, 1.0, 0.5, -1.0)
+
+
+@pytest.mark.parametrize("name", names(("idw", "sibson", "edge")))
+def test_oracle_matches_reference(name):
+    g = load(name)
+    U, V, W = cpu_ref.interp_grid(g["points"], g["values"], g["ax"], g["ay"], g["az"],
+                                  method=str(g["method"]), k=int(g["k"]), power=float(g["power"]))
+    for a, b in ((U, g["U"]), (V, g["V"]), (W, g["W"])):
+        if _bit_exact_expected(g) or str(g["method"]) == "sibson" and not int(g.get("tied", 0)):
+            # Sibson uses np.exp on the same machine class; exact here, normwise elsewhere.
+            assert normwise(a, b) <= 1e-13
+        if _bit_exact_expected(g):
+            assert np.array_equal(a, b, equal_nan=True)
+        assert normwise(a, b) <= 1e-10
+
+
+def test_oracle_masked_pipeline():
+    g = load("masked_spherepack_idw")
+    U, V, W = cpu_ref.interp_grid(g["points"], g["values"], g["ax"], g["ay"], g["az"], "idw", 8, 2.0)
+    assert normwise(U, g["U_raw"]) <= 1e-12
+    U, V, W = cpu_ref.nan_fill_and_mask(U, V, W, g["mask"])
+    for a, b in ((U, g["U"]), (V, g["V"]), (W, g["W"])):
+        assert normwise(a, b) <= 1e-12
+
+
+@pytest.mark.parametrize("k", [1, 3, 7, 8, 9, 16, 30, 50, 64, 127, 128, 129, 300])
+def test_pairwise_sum_matches_numpy(k):
+    rng = np.random.default_rng(k)
+    A = rng.standard_normal((300, k)) * np.exp(rng.uniform(-30, 30, (300, k)))
+    ref = A.sum(axis=1)
+    mine = np.array([cpu_ref.pairwise_sum(r) for r in A])
+    assert np.array_equal(ref, mine)
+
+
+def test_bruteforce_matches_kdtree():
+    rng = np.random.default_rng(3)
+    P = rng.uniform(0, 20, (3000, 3)); Qp = rng.uniform(-2, 22, (2000, 3))
+    d1, i1 = cpu_ref.knn_kdtree(P, Qp, 17)
+    d2, i2 = cpu_ref.knn_bruteforce(P, Qp, 17)
+    assert np.array_equal(d1, d2)
+    assert np.array_equal(i1, i2)
+
+
+def test_parallel_driver_equals_whole_grid():
+    g = load("idw_k8_p2")
+    U0, V0, W0 = cpu_ref.interp_grid(g["points"], g["values"], g["ax"], g["ay"], g["az"], "idw", 8, 2.0)
+    U1, V1, W1 = cpu_ref.interp_grid_parallel(g["points"], g["values"], g["ax"], g["ay"], g["az"], "idw", 8, 2.0, n_jobs=2)
+    assert np.array_equal(U0, U1) and np.array_equal(V0, V1) and np.array_equal(W0, W1)
