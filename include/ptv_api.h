@@ -87,15 +87,17 @@ typedef struct {
     const uint8_t *fluid_mask;
     uint32_t flags;      /* PTV_FLAG_* */
     double cell_occupancy; /* target particles per binning cell, <=0: default */
+    double r0_scale;       /* first search radius / expected k-NN radius, <=0: default */
+    int lattice_bounds;    /* >=0: coarse-lattice k-th distance bounds (default), <0: off */
 } ptv_knn_params;
 
 /* Per-call timings (ms, hipEvent based) and sizes. */
 typedef struct {
-    double ms_h2d, ms_bin, ms_knn, ms_d2h, ms_total;
+    double ms_h2d, ms_bin, ms_lattice, ms_knn, ms_d2h, ms_total;
     int64_t n_particles, n_voxels, n_cells;
     int32_t cells[3];
-    int32_t levels;
     double cell_size[3];
+    double r0;
 } ptv_stats;
 
 /* Library / device management. */
@@ -131,6 +133,14 @@ int ptv_interp_knn_dev(ptv_ctx *ctx, const ptv_particles *p, const ptv_grid *g,
  * kernel on the stream it ran on) and the synchronised phase stats.
  */
 int ptv_last_stats(ptv_ctx *ctx, ptv_stats *st);
+
+/*
+ * Diagnostics: mode 1 = enable + zero the k-NN traversal counters, 0 = disable,
+ * other = leave as is.  If out6 != NULL the (synchronised) totals are copied:
+ * {waves, nodes popped, nodes visited, leaves scanned, candidates, candidates
+ * accepted by at least one lane}.  Not thread-safe; for profiling only.
+ */
+int ptv_debug_counters(ptv_ctx *ctx, int mode, unsigned long long *out6);
 
 #ifdef __cplusplus
 }

@@ -45,14 +45,16 @@ class Grid(C.Structure):
 
 class KnnParams(C.Structure):
     _fields_ = [("method", C.c_int), ("k", C.c_int), ("power", C.c_double), ("eps", C.c_double),
-                ("fluid_mask", C.POINTER(C.c_uint8)), ("flags", C.c_uint32), ("cell_occupancy", C.c_double)]
+                ("fluid_mask", C.POINTER(C.c_uint8)), ("flags", C.c_uint32), ("cell_occupancy", C.c_double),
+                ("r0_scale", C.c_double), ("lattice_bounds", C.c_int)]
 
 
 class Stats(C.Structure):
-    _fields_ = [("ms_h2d", C.c_double), ("ms_bin", C.c_double), ("ms_knn", C.c_double), ("ms_d2h", C.c_double),
+    _fields_ = [("ms_h2d", C.c_double), ("ms_bin", C.c_double), ("ms_lattice", C.c_double), ("ms_knn", C.c_double),
+                ("ms_d2h", C.c_double),
                 ("ms_total", C.c_double), ("n_particles", C.c_int64), ("n_voxels", C.c_int64),
-                ("n_cells", C.c_int64), ("cells", C.c_int32 * 3), ("levels", C.c_int32),
-                ("cell_size", C.c_double * 3)]
+                ("n_cells", C.c_int64), ("cells", C.c_int32 * 3), ("cell_size", C.c_double * 3),
+                ("r0", C.c_double)]
 
     def as_dict(self):
         d = {f: getattr(self, f) for f, _ in self._fields_}
@@ -72,6 +74,7 @@ EXPORTS = {
     "ptv_interp_knn_dev": (C.c_int, [C.c_void_p, C.POINTER(Particles), C.POINTER(Grid), C.POINTER(KnnParams),
                                      _dp, _dp, _dp, C.c_void_p, C.POINTER(Stats)]),
     "ptv_last_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
+    "ptv_debug_counters": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_uint64)]),
 }
 
 _lib = None
@@ -162,9 +165,17 @@ class Context:
         check(lib().ptv_last_stats(self.h, C.byref(st)))
         return st.as_dict()
 
+    def debug_counters(self, mode=2):
+        """mode 1: enable+zero, 0: disable, 2: read. Returns the six traversal totals."""
+        out = (C.c_uint64 * 6)()
+        check(lib().ptv_debug_counters(self.h, int(mode), out))
+        keys = ("waves", "passes", "rounds", "candidates", "accepted", "rows")
+        return dict(zip(keys, list(out)))
+
     # -- host buffers ------------------------------------------------------
     def interp_knn(self, points, values, axes=None, grid_points=None, shape=None, method=METHOD_IDW, k=8,
-                   power=2.0, eps=1e-10, fluid_mask=None, flags=0, z_range=None, cell_occupancy=0.0):
+                   power=2.0, eps=1e-10, fluid_mask=None, flags=0, z_range=None, cell_occupancy=0.0,
+                   r0_scale=0.0, lattice_bounds=0):
         """Host-array k-NN interpolation. Returns (U, V, W) float64 (nz', ny, nx)."""
         pts = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 3)
         vals = np.ascontiguousarray(values, dtype=np.float64).reshape(-1, 3)
@@ -189,7 +200,7 @@ class Context:
             keep.append(mk)
         prm = KnnParams(method, int(k), float(power), float(eps),
                         mk.ctypes.data_as(C.POINTER(C.c_uint8)) if mk is not None else None, flags,
-                        float(cell_occupancy))
+                        float(cell_occupancy), float(r0_scale), int(lattice_bounds))
         out = [np.empty((z1 - z0, ny, nx), dtype=np.float64) for _ in range(3)]
         st = Stats()
         check(lib().ptv_interp_knn(self.h, C.byref(P), C.byref(G), C.byref(prm),
@@ -200,7 +211,7 @@ class Context:
     # -- device buffers (integer device pointers, e.g. torch tensor data_ptr()) --
     def interp_knn_dev(self, n, pptrs, nx, ny, nz, axes_ptrs=None, point_ptrs=None, out_ptrs=None,
                        method=METHOD_IDW, k=8, power=2.0, eps=1e-10, mask_ptr=0, flags=0, z_range=None,
-                       stream=0, cell_occupancy=0.0):
+                       stream=0, cell_occupancy=0.0, r0_scale=0.0, lattice_bounds=0):
         P = Particles(int(n), *[dev_dp(p) for p in pptrs])
         if axes_ptrs is not None:
             G = Grid(nx, ny, nz, *[dev_dp(p) for p in axes_ptrs], None, None, None, 0, nz)
@@ -210,7 +221,7 @@ class Context:
         G.z_begin, G.z_end = z0, z1
         prm = KnnParams(method, int(k), float(power), float(eps),
                         C.cast(C.c_void_p(mask_ptr), C.POINTER(C.c_uint8)) if mask_ptr else None, flags,
-                        float(cell_occupancy))
+                        float(cell_occupancy), float(r0_scale), int(lattice_bounds))
         st = Stats()
         check(lib().ptv_interp_knn_dev(self.h, C.byref(P), C.byref(G), C.byref(prm),
                                        *[dev_dp(p) for p in out_ptrs], C.c_void_p(stream or 0), C.byref(st)))

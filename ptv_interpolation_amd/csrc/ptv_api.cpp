@@ -50,16 +50,20 @@ struct DevBuf {
 
 using namespace ptv;
 
+static constexpr int kMaxLattice = 6;
+
 struct ptv_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipEvent_t ev_knn0 = nullptr, ev_knn1 = nullptr, ev_bin0 = nullptr, ev_bin1 = nullptr;
+    hipEvent_t ev_knn0 = nullptr, ev_knn1 = nullptr, ev_bin0 = nullptr, ev_bin1 = nullptr, ev_lat1 = nullptr;
     bool timed_pending = false;
     DevBuf<double> pin[6], axes, qpts[3], out[3];
     DevBuf<uint8_t> mask;
     DevBuf<uint32_t> code, perm, count, start, scanp;
     DevBuf<double4> prec, pval;
     DevBuf<double> bbox_part, bbox_out;
+    DevBuf<unsigned long long> dbg;
+    DevBuf<double> lat_axes[kMaxLattice], lat_dk[kMaxLattice];  // coarse-lattice bound levels
     double *h_bbox = nullptr;  // pinned, 6 doubles
     ptv_stats last{};
 };
@@ -108,6 +112,7 @@ int ptv_init(int device, ptv_ctx **out) {
     PTV_HIP(hipEventCreate(&c->ev_knn1));
     PTV_HIP(hipEventCreate(&c->ev_bin0));
     PTV_HIP(hipEventCreate(&c->ev_bin1));
+    PTV_HIP(hipEventCreate(&c->ev_lat1));
     PTV_HIP(hipHostMalloc(&c->h_bbox, 8 * sizeof(double)));
     *out = c;
     return PTV_OK;
@@ -131,11 +136,16 @@ int ptv_free(ptv_ctx *c) {
     c->pval.release();
     c->bbox_part.release();
     c->bbox_out.release();
+    if (ptv::g_dbg == c->dbg.p) ptv::g_dbg = nullptr;
+    c->dbg.release();
+    for (auto &b : c->lat_axes) b.release();
+    for (auto &b : c->lat_dk) b.release();
     if (c->h_bbox) hipHostFree(c->h_bbox);
     hipEventDestroy(c->ev_knn0);
     hipEventDestroy(c->ev_knn1);
     hipEventDestroy(c->ev_bin0);
     hipEventDestroy(c->ev_bin1);
+    hipEventDestroy(c->ev_lat1);
     hipStreamDestroy(c->stream);
     delete c;
     return PTV_OK;
@@ -144,6 +154,12 @@ int ptv_free(ptv_ctx *c) {
 }  // extern "C"
 
 namespace {
+
+constexpr double kDefaultOccupancy = 0.35;  // particles per binning cell
+constexpr double kDefaultR0Scale = 1.0;     // first gather radius / expected k-NN radius
+constexpr long long kMaxCells = 1LL << 28;
+constexpr int kLatticeStep = 4;                 // coarse lattice = every 4th grid point (+ last)
+constexpr long long kLatticeStopPoints = 50000; // no coarser lattice below this many points
 
 int validate(const ptv_particles *p, const ptv_grid *g, const ptv_knn_params *prm) {
     if (!p || !g || !prm) {
@@ -194,16 +210,15 @@ int validate(const ptv_particles *p, const ptv_grid *g, const ptv_knn_params *pr
 // Cell grid over the union bounding box: ~`occ` particles per cell on average.
 CellGrid make_cell_grid(const double lo_in[3], const double hi_in[3], int64_t n, double occ) {
     CellGrid cg{};
-    double ext[3], lo[3];
+    double ext[3];
     double maxext = 0.0, maxabs = 0.0;
     for (int a = 0; a < 3; ++a) {
-        lo[a] = lo_in[a];
         ext[a] = hi_in[a] - lo_in[a];
         if (!(ext[a] > 0.0)) ext[a] = 0.0;
         maxext = std::max(maxext, ext[a]);
         maxabs = std::max(maxabs, std::max(std::fabs(lo_in[a]), std::fabs(hi_in[a])));
     }
-    if (!(occ > 0.0)) occ = 3.0;
+    if (!(occ > 0.0)) occ = kDefaultOccupancy;
     double vol = 1.0;
     int dims = 0;
     for (int a = 0; a < 3; ++a)
@@ -212,24 +227,42 @@ CellGrid make_cell_grid(const double lo_in[3], const double hi_in[3], int64_t n,
             ++dims;
         }
     double cs = dims ? std::pow(occ * vol / (double)n, 1.0 / dims) : 1.0;
-    int maxnc = 1;
-    for (int a = 0; a < 3; ++a) {
-        int nc = 1;
-        if (ext[a] > 1e-9 * maxext && cs > 0.0) {
-            double f = std::ceil(ext[a] / cs);
-            nc = (int)std::min(512.0, std::max(1.0, f));
+    for (int iter = 0; iter < 64; ++iter) {  // cap the cell count (memory) by growing cs
+        long long tot = 1;
+        for (int a = 0; a < 3; ++a) {
+            int nc = 1;
+            if (ext[a] > 1e-9 * maxext && cs > 0.0) nc = (int)std::max(1.0, std::min(1e6, std::ceil(ext[a] / cs)));
+            cg.nc[a] = nc;
+            tot *= nc;
         }
-        cg.nc[a] = nc;
-        maxnc = std::max(maxnc, nc);
-        cg.cs[a] = ext[a] > 0.0 ? ext[a] / nc : 1.0;
-        cg.ic[a] = 1.0 / cg.cs[a];
-        cg.o[a] = lo[a];
-        cg.mg[a] = 1e-12 * (maxabs + maxext) + 1e-12 * cg.cs[a];
+        cg.ncells = tot;
+        if (tot <= kMaxCells) break;
+        cs *= 1.1;
     }
-    int L = 0;
-    while ((1 << L) < maxnc) ++L;
-    cg.L = L;
+    for (int a = 0; a < 3; ++a) {
+        cg.cs[a] = ext[a] > 0.0 ? ext[a] / cg.nc[a] : 1.0;
+        cg.ic[a] = 1.0 / cg.cs[a];
+        cg.o[a] = lo_in[a];
+    }
+    cg.mg = 1e-12 * (maxabs + maxext) + 1e-300;
     return cg;
+}
+
+// First gather radius: the radius of a ball expected to hold k particles at the mean
+// density of the bounding box, times `scale` (every lane's k-th distance usually fits).
+double first_radius(const double lo[3], const double hi[3], int64_t n, int k, double scale) {
+    if (!(scale > 0.0)) scale = kDefaultR0Scale;
+    double vol = 1.0, maxext = 0.0;
+    int dims = 0;
+    for (int a = 0; a < 3; ++a) maxext = std::max(maxext, hi[a] - lo[a]);
+    for (int a = 0; a < 3; ++a)
+        if (hi[a] - lo[a] > 1e-9 * maxext) {
+            vol *= hi[a] - lo[a];
+            ++dims;
+        }
+    if (dims == 0 || maxext <= 0.0) return 1.0;
+    const double unit = dims == 3 ? 4.18879020478639 : (dims == 2 ? 3.14159265358979 : 2.0);
+    return scale * std::pow((double)k * vol / ((double)n * unit), 1.0 / dims);
 }
 
 int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn_params *prm, const double *ax,
@@ -275,8 +308,7 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
 
     // 2. binning
     CellGrid cg = make_cell_grid(lo, hi, n, prm->cell_occupancy);
-    const size_t P = (size_t)1 << cg.L;
-    const size_t m = P * P * P;
+    const size_t m = (size_t)cg.ncells;
     PTV_TRY(c->code.ensure(n));
     PTV_TRY(c->perm.ensure(n));
     PTV_TRY(c->prec.ensure(n));
@@ -289,7 +321,40 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
                        c->pval.p, s));
     PTV_HIP(hipEventRecord(c->ev_bin1, s));
 
-    // 3. k-NN interpolation
+    // 3. coarse-lattice k-th distance bounds (separable grids): every 4th point of the
+    //    grid, recursively, down to a few tens of thousands of points; each level is an
+    //    exact k-NN pass (k-th distance only) bounded by the next coarser level.
+    struct Lat {
+        int n[3];
+        double *ax, *ay, *az, *dk;
+    };
+    Lat lat[kMaxLattice];
+    int nlat = 0;
+    if (sep && prm->lattice_bounds >= 0) {
+        int n[3] = {(int)g->nx, (int)g->ny, (int)(z1 - z0)};
+        const double *src[3] = {ax, ay, az + z0};
+        while (nlat < kMaxLattice) {
+            const long long pts = (long long)n[0] * n[1] * n[2];
+            if (pts <= kLatticeStopPoints || std::min(n[0], std::min(n[1], n[2])) < 9) break;
+            Lat &L = lat[nlat];
+            for (int d = 0; d < 3; ++d) L.n[d] = n[d] <= 1 ? 1 : (n[d] - 1 + kLatticeStep - 1) / kLatticeStep + 1;
+            PTV_TRY(c->lat_axes[nlat].ensure((size_t)L.n[0] + L.n[1] + L.n[2]));
+            PTV_TRY(c->lat_dk[nlat].ensure((size_t)L.n[0] * L.n[1] * L.n[2]));
+            L.ax = c->lat_axes[nlat].p;
+            L.ay = L.ax + L.n[0];
+            L.az = L.ay + L.n[1];
+            L.dk = c->lat_dk[nlat].p;
+            double *dst[3] = {L.ax, L.ay, L.az};
+            for (int d = 0; d < 3; ++d) PTV_TRY(launch_subsample(src[d], n[d], kLatticeStep, dst[d], L.n[d], s));
+            for (int d = 0; d < 3; ++d) {
+                src[d] = dst[d];
+                n[d] = L.n[d];
+            }
+            ++nlat;
+        }
+    }
+
+    // 4. k-NN interpolation
     KnnLaunch kl;
     kl.cg = cg;
     kl.nx = (int)g->nx;
@@ -303,8 +368,39 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
     kl.power = prm->power;
     kl.eps = prm->eps;
     kl.flags = prm->flags;
+    kl.r0 = first_radius(lo, hi, n, prm->k, prm->r0_scale);
     Binned b{c->prec.p, c->pval.p, c->start.p, n};
     PTV_HIP(hipEventRecord(c->ev_knn0, s));
+    for (int l = nlat - 1; l >= 0; --l) {  // coarsest first
+        KnnLaunch ll = kl;
+        ll.nx = lat[l].n[0];
+        ll.ny = lat[l].n[1];
+        ll.nz = lat[l].n[2];
+        ll.z0 = 0;
+        ll.z1 = lat[l].n[2];
+        ll.mode = kModeKDist;
+        ll.flags = 0;
+        ll.point_per_wave = (l == nlat - 1) ? 1 : 0;
+        if (l + 1 < nlat) {
+            ll.cb.ax = lat[l + 1].ax;
+            ll.cb.ay = lat[l + 1].ay;
+            ll.cb.az = lat[l + 1].az;
+            ll.cb.dk = lat[l + 1].dk;
+            for (int d = 0; d < 3; ++d) ll.cb.n[d] = lat[l + 1].n[d];
+            ll.cb.step = kLatticeStep;
+        }
+        PTV_TRY(launch_knn(ll, b, lat[l].ax, lat[l].ay, lat[l].az, nullptr, nullptr, nullptr, nullptr, lat[l].dk,
+                           lat[l].dk, lat[l].dk, s));
+    }
+    if (nlat > 0) {
+        kl.cb.ax = lat[0].ax;
+        kl.cb.ay = lat[0].ay;
+        kl.cb.az = lat[0].az;
+        kl.cb.dk = lat[0].dk;
+        for (int d = 0; d < 3; ++d) kl.cb.n[d] = lat[0].n[d];
+        kl.cb.step = kLatticeStep;
+    }
+    PTV_HIP(hipEventRecord(c->ev_lat1, s));
     PTV_TRY(launch_knn(kl, b, ax, ay, az, qx, qy, qz, mask, U, V, W, s));
     PTV_HIP(hipEventRecord(c->ev_knn1, s));
     c->timed_pending = true;
@@ -318,7 +414,7 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
         ls.cells[a] = cg.nc[a];
         ls.cell_size[a] = cg.cs[a];
     }
-    ls.levels = cg.L;
+    ls.r0 = kl.r0;
     if (st) *st = ls;
     return PTV_OK;
 }
@@ -327,8 +423,10 @@ int finish_timing(ptv_ctx *c) {
     if (!c->timed_pending) return PTV_OK;
     PTV_HIP(hipEventSynchronize(c->ev_knn1));
     float ms = 0.f;
-    PTV_HIP(hipEventElapsedTime(&ms, c->ev_knn0, c->ev_knn1));
+    PTV_HIP(hipEventElapsedTime(&ms, c->ev_lat1, c->ev_knn1));
     c->last.ms_knn = ms;
+    PTV_HIP(hipEventElapsedTime(&ms, c->ev_knn0, c->ev_lat1));
+    c->last.ms_lattice = ms;
     PTV_HIP(hipEventElapsedTime(&ms, c->ev_bin0, c->ev_bin1));
     c->last.ms_bin = ms;
     c->timed_pending = false;
@@ -440,6 +538,27 @@ int ptv_interp_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const 
     hipEventDestroy(t2);
     hipEventDestroy(t3);
     if (st) *st = c->last;
+    return PTV_OK;
+}
+
+int ptv_debug_counters(ptv_ctx *c, int mode, unsigned long long *out6) {
+    if (!c) {
+        set_error("NULL context");
+        return PTV_E_ARG;
+    }
+    PTV_HIP(hipSetDevice(c->device));
+    if (mode == 1) {  // enable + zero
+        PTV_TRY(c->dbg.ensure(8));
+        PTV_HIP(hipMemsetAsync(c->dbg.p, 0, 8 * sizeof(unsigned long long), c->stream));
+        PTV_HIP(hipStreamSynchronize(c->stream));
+        ptv::g_dbg = c->dbg.p;
+    } else if (mode == 0) {
+        ptv::g_dbg = nullptr;
+    }
+    if (out6 && c->dbg.p) {
+        PTV_HIP(hipDeviceSynchronize());
+        PTV_HIP(hipMemcpy(out6, c->dbg.p, 6 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    }
     return PTV_OK;
 }
 

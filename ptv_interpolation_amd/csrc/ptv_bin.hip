@@ -2,12 +2,12 @@
 //
 // Replaces the role of the per-call cKDTree build in the reference
 // (interpolator.py:90 and :132, scipy KDTree(points), leafsize 10): particles
-// are counting-sorted into a uniform cell grid addressed by Morton code on a
-// padded 2^L cube, so that every octree node is a contiguous particle range.
+// are counting-sorted into a uniform cell grid in linear (z, y, x) order, so
+// that every x-run of cells in a row is one contiguous particle range.
 //
 //   bbox        per-axis min/max of particles and queries (grid-stride, LDS reduce)
-//   cell_code   Morton code per particle + atomic histogram
-//   scan        exclusive prefix sum of the P^3 histogram (3-phase, 4096 cells/block)
+//   cell_code   linear cell id per particle + atomic histogram
+//   scan        exclusive prefix sum of the cell histogram (3-phase, 4096 cells/block)
 //   scatter     particle -> slot (atomic fill from the back of each cell)
 //   seg_sort    ascending original index inside each cell (deterministic order)
 //   gather      AoS records for the scalar-load k-NN kernel:
@@ -125,7 +125,7 @@ __global__ __launch_bounds__(256) void k_cell_code(CellGrid cg, const double *__
     int cx = cell_coord(x[i], cg.o[0], cg.ic[0], cg.nc[0]);
     int cy = cell_coord(y[i], cg.o[1], cg.ic[1], cg.nc[1]);
     int cz = cell_coord(z[i], cg.o[2], cg.ic[2], cg.nc[2]);
-    uint32_t c = morton3((uint32_t)cx, (uint32_t)cy, (uint32_t)cz);
+    uint32_t c = (uint32_t)(((long long)cz * cg.nc[1] + cy) * cg.nc[0] + cx);
     code[i] = c;
     atomicAdd(&count[c], 1u);
 }
@@ -299,8 +299,7 @@ __global__ __launch_bounds__(256) void k_gather(const uint32_t *__restrict__ per
 int launch_bin(const CellGrid &cg, const double *const px[3], const double *const pv[3], int64_t n,
                uint32_t *d_code, uint32_t *d_perm, uint32_t *d_count, uint32_t *d_start,
                uint32_t *d_scan_partials, double4 *d_prec, double4 *d_pval, hipStream_t s) {
-    const size_t P = (size_t)1 << cg.L;
-    const size_t m = P * P * P;
+    const size_t m = (size_t)cg.ncells;
     PTV_HIP(hipMemsetAsync(d_count, 0, m * sizeof(uint32_t), s));
     const int nb = (int)((n + 255) / 256);
     hipLaunchKernelGGL(k_cell_code, dim3(nb), dim3(256), 0, s, cg, px[0], px[1], px[2], n, d_code, d_count);

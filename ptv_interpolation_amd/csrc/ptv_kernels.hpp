@@ -11,9 +11,9 @@ namespace ptv {
 int launch_bbox(const double *const px[3], int64_t n, const double *const qa[3], const int64_t qn[3],
                 double *d_partials, int max_blocks, double *d_out6, hipStream_t s);
 
-// Counting-sort the particles into Morton-ordered cells (deterministic order
+// Counting-sort the particles into linear-order cells (deterministic order
 // inside each cell: ascending original index).  Scratch buffers must hold
-// n entries (code, perm) and P^3 (+1) entries (count, start).
+// n entries (code, perm) and ncells (+1) entries (count, start).
 int launch_bin(const CellGrid &cg, const double *const px[3], const double *const pv[3], int64_t n,
                uint32_t *d_code, uint32_t *d_perm, uint32_t *d_count, uint32_t *d_start,
                uint32_t *d_scan_partials, double4 *d_prec, double4 *d_pval, hipStream_t s);
@@ -21,6 +21,19 @@ int launch_bin(const CellGrid &cg, const double *const px[3], const double *cons
 size_t scan_partials_needed(size_t m);
 
 // ---- k-NN interpolation (ptv_knn.hip) ----
+// Exact k-th-neighbour distances on a coarser separable lattice (every `step`-th
+// point of this launch's grid, plus the last): d_k(v) <= dk(c) + |v - c| for any
+// lattice point c bounds every voxel's search radius (triangle inequality).
+struct CoarseBound {
+    const double *ax = nullptr, *ay = nullptr, *az = nullptr;  // lattice axes
+    const double *dk = nullptr;                                // (n[2], n[1], n[0]) k-th distances
+    int n[3] = {0, 0, 0};
+    int step = 4;
+};
+
+constexpr int kModeInterp = 0;  // write U, V, W
+constexpr int kModeKDist = 1;   // write the exact k-th neighbour distance into U
+
 struct KnnLaunch {
     CellGrid cg;
     int nx, ny, nz;      // full grid
@@ -30,9 +43,17 @@ struct KnnLaunch {
     int k;
     double power, eps;
     uint32_t flags;
+    double r0;           // first gather radius (from the mean particle density)
+    int mode = kModeInterp;
+    int point_per_wave = 0;  // 1: one grid point per wave (coarsest lattice)
+    CoarseBound cb;
 };
 
+// out[j] = in[min(step*j, n-1)] for j < nout (lattice axes)
+int launch_subsample(const double *in, int n, int step, double *out, int nout, hipStream_t s);
+
 int kmax_for(int k);  // compile-time list length serving k, 0 if unsupported
+extern unsigned long long *g_dbg;  // traversal counters (diagnostics), NULL = off
 
 int launch_knn(const KnnLaunch &a, const Binned &b, const double *ax, const double *ay, const double *az,
                const double *qx, const double *qy, const double *qz, const uint8_t *mask, double *U, double *V,

@@ -6,21 +6,30 @@
 //   (Sibson: inv-distance * exp(-d/std(d)), renormalised            interpolator.py:102-116)
 //   out[:, c] = (weights * values[indices, c]).sum(axis=1)          interpolator.py:150-153 (:119-122)
 //
-// Work decomposition: one wave64 = one 4x4x4 voxel tile (lane = voxel), a 256-thread
-// workgroup = 4 tiles along x (16x4x4 voxels: 128-B output rows).  Each wave walks the
-// Morton octree of particle cells front-to-back with a wave-uniform stack kept in one
-// VGPR (lane i = stack slot i; v_readlane pops, a lane-select pushes); a node is visited iff some
-// lane's voxel is closer to the node box than that lane's current k-th distance, so
-// voids (sphere interiors) cost a few node tests instead of a shell of empty cells.
-// Particle records are read with wave-uniform addresses (scalar loads), so each
-// candidate is one s_load shared by 64 voxels; per lane a sorted register list of the
-// KMAX best (d2, slot) is kept by a branch-free insertion network.
+// Work decomposition: one wave64 = one 4x4x4 voxel tile (lane = voxel); a 256-thread
+// workgroup = 4 independent tiles along x (16x4x4 voxels, 128-B output rows).
+//
+// Exact search by radius shells around the tile's bounding box B:
+//   pass 1 gathers every particle whose cell lies within R0 of B (R0 from the mean
+//   particle density); pass j gathers the shell R_{j-1} < dist <= R_j.  A lane whose
+//   current k-th distance is <= R_j is exact (every particle it has not seen is
+//   farther than R_j from B, hence from its voxel).  If all lists are full the next
+//   radius is the largest lane k-th distance (one more pass finishes every lane);
+//   otherwise R doubles.  Sphere interiors (empty voids) just take more passes.
+// Gather: the candidate cells of a pass are, per cell row (cy, cz), one or two x-runs
+// of consecutive cells = contiguous particle ranges of the linear-order counting sort.
+// Lane i takes row i: it loads its run bounds from cell_start (64 rows per round,
+// all loads in flight together), a wave prefix sum places the runs, and the lanes
+// copy the particle records into a per-wave LDS buffer.  The compute loop then reads
+// each candidate with a wave-uniform LDS address (broadcast) and updates every lane's
+// sorted register list of the KMAX best (d2, slot) with a branch-free insertion
+// network, skipped wave-wide when no lane improves.
 //
 // Bit-level contract with the reference (compiled with -ffp-contract=off):
 //   d2 = (dx*dx + dy*dy) + dz*dz, d = sqrt(d2)      (cKDTree p=2 accumulation, then sqrt)
 //   d**p: p=2 -> d*d, 1 -> d, 0.5 -> sqrt, -1 -> 1/d, else pow (numpy scalar fast paths)
 //   row sums: numpy pairwise order from identity 0.0 (8 accumulators, n%8 tail)
-// Ties at equal d2 keep the earlier candidate in the fixed traversal order
+// Ties at equal d2 keep the earlier candidate in the (deterministic) gather order
 // (cKDTree's tie order is traversal dependent too).
 #include <hip/hip_runtime.h>
 
@@ -32,7 +41,12 @@
 
 namespace ptv {
 
-constexpr int kLeafMax = 16;  // a node with <= kLeafMax particles is scanned directly
+constexpr int kCap = 256;        // LDS candidate slots per wave (32 B each)
+constexpr int kRowsPerLane = 2;  // cell rows examined per lane per gather round
+constexpr int kRunEntries = 64 * 2 * kRowsPerLane;  // x-runs per gather round (power of two)
+
+// optional per-launch search counters (device buffer of 6 u64), see ptv_debug_counters()
+unsigned long long *g_dbg = nullptr;
 
 struct KnnKernelArgs {
     CellGrid cg;
@@ -41,6 +55,11 @@ struct KnnKernelArgs {
     int separable, method, k, kpad;
     double power, eps;
     uint32_t flags;
+    double r0;    // first gather radius
+    double rall;  // radius that covers the whole cell grid from any query
+    int mode;     // kModeInterp / kModeKDist
+    int point_per_wave;
+    CoarseBound cb;
 };
 
 // numpy pairwise sum of a[0..n) (n <= KMAX <= 128), from identity 0.0.
@@ -104,6 +123,27 @@ __device__ __forceinline__ double wave_max(double v) {
     for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
     return v;
 }
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ int wave_incl_scan_i(int v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+// order this wave's LDS writes before its later reads (and vice versa)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 template <int KMAX>
 __device__ __forceinline__ void insert(double (&bd)[KMAX], int (&bp)[KMAX], double d2, int p) {
@@ -125,6 +165,17 @@ __device__ __forceinline__ void insert(double (&bd)[KMAX], int (&bp)[KMAX], doub
     }
 }
 
+__device__ __forceinline__ int clampi(double f, int n) {
+    return f < 0.0 ? 0 : (f >= (double)(n - 1) ? n - 1 : (int)f);
+}
+
+// distance between the extent [lo, hi] of a query box and cell c of an axis
+__device__ __forceinline__ double axis_gap(int c, double o, double cs, double lo, double hi) {
+    const double c0 = o + (double)c * cs;
+    const double c1 = o + (double)(c + 1) * cs;
+    return fmax(fmax(c0 - hi, lo - c1), 0.0);
+}
+
 template <int KMAX>
 __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const double4 *__restrict__ prec,
                                                     const double4 *__restrict__ pval,
@@ -133,21 +184,36 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
                                                     const double *__restrict__ az, const double *__restrict__ qpx,
                                                     const double *__restrict__ qpy, const double *__restrict__ qpz,
                                                     const uint8_t *__restrict__ mask, double *__restrict__ U,
-                                                    double *__restrict__ V, double *__restrict__ W) {
+                                                    double *__restrict__ V, double *__restrict__ W,
+                                                    unsigned long long *__restrict__ dbg) {
+    __shared__ double4 lds_cand[4][kCap];
+    __shared__ uint2 lds_runs[4][kRunEntries];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
+    double4 *buf = lds_cand[wid];
+    uint2 *runs = lds_runs[wid];
     const int b = blockIdx.x;
-    const int bx = b % a.ntxb;
-    const int rr = b / a.ntxb;
-    const int ty = rr % a.nty;
-    const int tz = rr / a.nty;
-    const int tx = bx * 4 + wid;
-    if (tx >= a.ntx) return;  // wave-uniform
-
-    const int ix = tx * 4 + (lane & 3);
-    const int iy = ty * 4 + ((lane >> 2) & 3);
-    const int iz = a.z0 + tz * 4 + (lane >> 4);
-    const bool valid = ix < a.nx && iy < a.ny && iz < a.z1;
+    int ix, iy, iz;
+    if (a.point_per_wave) {
+        // every lane of the wave takes the same grid point (coarsest lattice: a point-sized
+        // box keeps each wave's candidate set small however sparse the lattice is)
+        const long long gp = (long long)b * 4 + wid;
+        if (gp >= (long long)a.nx * a.ny * (a.z1 - a.z0)) return;  // wave-uniform
+        ix = (int)(gp % a.nx);
+        iy = (int)((gp / a.nx) % a.ny);
+        iz = a.z0 + (int)(gp / ((long long)a.nx * a.ny));
+    } else {
+        const int bx = b % a.ntxb;
+        const int rr = b / a.ntxb;
+        const int ty = rr % a.nty;
+        const int tz = rr / a.nty;
+        const int tx = bx * 4 + wid;
+        if (tx >= a.ntx) return;  // wave-uniform
+        ix = tx * 4 + (lane & 3);
+        iy = ty * 4 + ((lane >> 2) & 3);
+        iz = a.z0 + tz * 4 + (lane >> 4);
+    }
+    const bool valid = ix < a.nx && iy < a.ny && iz < a.z1 && (!a.point_per_wave || lane == 0);
     const int cx = min(ix, a.nx - 1), cy = min(iy, a.ny - 1), cz = min(iz, a.z1 - 1);
     const size_t vfull = ((size_t)cz * a.ny + cy) * a.nx + cx;
     double qx, qy, qz;
@@ -160,72 +226,192 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
         qy = qpy[vfull];
         qz = qpz[vfull];
     }
-    const bool active = valid && (mask == nullptr || mask[vfull] != 0);
+    const bool active = (valid || a.point_per_wave) && (mask == nullptr || mask[vfull] != 0);
 
-    // sorted list: KMAX-k front sentinels (-1) so bd[KMAX-1] is the k-th best
+    // upper bound on this voxel's k-th distance from the coarse lattice (triangle inequality)
+    double ub = INFINITY;
+    if (a.cb.dk != nullptr && active) {
+        const int st = a.cb.step;
+        const int j0[3] = {cx / st, cy / st, (cz - a.z0) / st};
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const int jx = min(j0[0] + (c & 1), a.cb.n[0] - 1);
+            const int jy = min(j0[1] + ((c >> 1) & 1), a.cb.n[1] - 1);
+            const int jz = min(j0[2] + (c >> 2), a.cb.n[2] - 1);
+            const double ex = qx - a.cb.ax[jx], ey = qy - a.cb.ay[jy], ez = qz - a.cb.az[jz];
+            const double D = a.cb.dk[((size_t)jz * a.cb.n[1] + jy) * a.cb.n[0] + jx];
+            ub = fmin(ub, D + sqrt((ex * ex + ey * ey) + ez * ez));
+        }
+        ub = ub * (1.0 + 1e-12) + a.cg.mg;
+    }
+    // candidates at or beyond the bound can never be among the k nearest
+    const double ub2 = !active ? -1.0 : (ub < INFINITY ? ub * ub : INFINITY);
+
+    // sorted list: KMAX-k front sentinels (-1) so bd[KMAX-1] is the k-th best.
+    // Inactive lanes (padding / solid voxels) hold -1 everywhere: they never accept a
+    // candidate and never ask for a larger radius.
     double bd[KMAX];
     int bp[KMAX];
 #pragma unroll
     for (int j = 0; j < KMAX; ++j) {
-        bd[j] = (j < a.kpad) ? -1.0 : INFINITY;
+        bd[j] = (!active || j < a.kpad) ? -1.0 : INFINITY;
         bp[j] = -1;
     }
-    double thr = active ? INFINITY : -1.0;
+    double thr = fmin(bd[KMAX - 1], ub2);
+    uint32_t n_pass = 0, n_round = 0, n_rows = 0, n_cand = 0, n_acc = 0;
 
     if (__builtin_amdgcn_ballot_w64(active) != 0) {
-        // tile centre (front-to-back child order)
-        const double tcx = 0.5 * (wave_min(active ? qx : INFINITY) + wave_max(active ? qx : -INFINITY));
-        const double tcy = 0.5 * (wave_min(active ? qy : INFINITY) + wave_max(active ? qy : -INFINITY));
-        const double tcz = 0.5 * (wave_min(active ? qz : INFINITY) + wave_max(active ? qz : -INFINITY));
-        const int L = a.cg.L;
-        int stack = 0;
-        stack = (lane == 0) ? (int)((uint32_t)L << 27) : stack;
-        int sp = 1;
-        while (sp > 0) {
-            --sp;
-            const uint32_t e = (uint32_t)__builtin_amdgcn_readlane(stack, sp);
-            const int l = (int)(e >> 27);
-            const uint32_t code = e & ((1u << 27) - 1u);
-            const uint32_t s0 = cstart[code << (3 * l)];
-            const uint32_t s1 = cstart[(code + 1u) << (3 * l)];
-            if (s0 == s1) continue;
-            const uint32_t ci = compact3(code), cj = compact3(code >> 1), ck = compact3(code >> 2);
-            const double x0 = a.cg.o[0] + (double)(ci << l) * a.cg.cs[0] - a.cg.mg[0];
-            const double x1 = a.cg.o[0] + (double)((ci + 1u) << l) * a.cg.cs[0] + a.cg.mg[0];
-            const double y0 = a.cg.o[1] + (double)(cj << l) * a.cg.cs[1] - a.cg.mg[1];
-            const double y1 = a.cg.o[1] + (double)((cj + 1u) << l) * a.cg.cs[1] + a.cg.mg[1];
-            const double z0 = a.cg.o[2] + (double)(ck << l) * a.cg.cs[2] - a.cg.mg[2];
-            const double z1 = a.cg.o[2] + (double)((ck + 1u) << l) * a.cg.cs[2] + a.cg.mg[2];
-            const double ddx = fmax(fmax(x0 - qx, qx - x1), 0.0);
-            const double ddy = fmax(fmax(y0 - qy, qy - y1), 0.0);
-            const double ddz = fmax(fmax(z0 - qz, qz - z1), 0.0);
-            const double md2 = (ddx * ddx + ddy * ddy) + ddz * ddz;
-            if (__builtin_amdgcn_ballot_w64(md2 < thr) == 0) continue;
-            if (l == 0 || s1 - s0 <= (uint32_t)kLeafMax) {
-                for (uint32_t p = s0; p < s1; ++p) {
-                    const double4 r = prec[p];
-                    const double dx = qx - r.x, dy = qy - r.y, dz = qz - r.z;
-                    const double d2 = (dx * dx + dy * dy) + dz * dz;
-                    if (d2 < thr) {
-                        insert<KMAX>(bd, bp, d2, (int)p);
-                        thr = bd[KMAX - 1];
+        const double bx0 = wave_min(active ? qx : INFINITY), bx1 = wave_max(active ? qx : -INFINITY);
+        const double by0 = wave_min(active ? qy : INFINITY), by1 = wave_max(active ? qy : -INFINITY);
+        const double bz0 = wave_min(active ? qz : INFINITY), bz1 = wave_max(active ? qz : -INFINITY);
+        const CellGrid &g = a.cg;
+        double Rp = -1.0;  // radius already gathered (none yet)
+        // R_ub covers every lane's k-th neighbour: small (fluid) -> try r0 first and then
+        // the exact max k-th distance; large (void) -> one pass at R_ub.
+        const double R_ub = wave_max(active ? ub : -INFINITY);
+        double R = a.r0;
+        if (R_ub < INFINITY) R = fmin(R_ub, a.r0);
+        int py0 = 1, py1 = 0, pz0 = 1, pz1 = 0;  // row box of the previous pass (empty)
+        while (true) {
+            ++n_pass;
+            const double Rg = R + g.mg, Rg2 = Rg * Rg;
+            const double Rpg2 = Rp < 0.0 ? -1.0 : (Rp + g.mg) * (Rp + g.mg);
+            const int ry0 = clampi(floor((by0 - Rg - g.o[1]) * g.ic[1]), g.nc[1]);
+            const int ry1 = clampi(floor((by1 + Rg - g.o[1]) * g.ic[1]), g.nc[1]);
+            const int rz0 = clampi(floor((bz0 - Rg - g.o[2]) * g.ic[2]), g.nc[2]);
+            const int rz1 = clampi(floor((bz1 + Rg - g.o[2]) * g.ic[2]), g.nc[2]);
+            const int nyr = ry1 - ry0 + 1;
+            const int nrows = nyr * (rz1 - rz0 + 1);
+            for (int rb = 0; rb < nrows; rb += 64 * kRowsPerLane) {
+                ++n_round;
+                // ---- lane = kRowsPerLane cell rows: x-runs of this shell -> particle ranges ----
+                uint32_t rs[2 * kRowsPerLane];
+                int rc[2 * kRowsPerLane];
+#pragma unroll
+                for (int q = 0; q < kRowsPerLane; ++q) {
+                    const int row = rb + q * 64 + lane;
+                    rs[2 * q] = rs[2 * q + 1] = 0;
+                    rc[2 * q] = rc[2 * q + 1] = 0;
+                    if (row < nrows) {
+                        const int ccy = ry0 + row % nyr, ccz = rz0 + row / nyr;
+                        const double gy = axis_gap(ccy, g.o[1], g.cs[1], by0, by1);
+                        const double gz = axis_gap(ccz, g.o[2], g.cs[2], bz0, bz1);
+                        const double h2 = gy * gy + gz * gz;
+                        if (h2 <= Rg2) {
+                            const double rx = sqrt(Rg2 - h2);
+                            const int a1 = clampi(floor((bx0 - rx - g.o[0]) * g.ic[0]), g.nc[0]);
+                            const int b1 = clampi(floor((bx1 + rx - g.o[0]) * g.ic[0]), g.nc[0]);
+                            int lo1 = a1, hi1 = b1, lo2 = 1, hi2 = 0;  // [lo, hi] inclusive runs
+                            if (h2 <= Rpg2 && ccy >= py0 && ccy <= py1 && ccz >= pz0 && ccz <= pz1) {
+                                // row was gathered by the previous pass: only the x extensions are new
+                                const double rxo = sqrt(Rpg2 - h2);
+                                const int a0 = clampi(floor((bx0 - rxo - g.o[0]) * g.ic[0]), g.nc[0]);
+                                const int b0 = clampi(floor((bx1 + rxo - g.o[0]) * g.ic[0]), g.nc[0]);
+                                hi1 = a0 - 1;
+                                lo2 = b0 + 1;
+                                hi2 = b1;
+                            }
+                            const long long rowbase = ((long long)ccz * g.nc[1] + ccy) * g.nc[0];
+                            if (lo1 <= hi1) {
+                                rs[2 * q] = cstart[rowbase + lo1];
+                                rc[2 * q] = (int)(cstart[rowbase + hi1 + 1] - rs[2 * q]);
+                            }
+                            if (lo2 <= hi2) {
+                                rs[2 * q + 1] = cstart[rowbase + lo2];
+                                rc[2 * q + 1] = (int)(cstart[rowbase + hi2 + 1] - rs[2 * q + 1]);
+                            }
+                            ++n_rows;
+                        }
                     }
                 }
-            } else {
-                const double mx = 0.5 * (x0 + x1), my = 0.5 * (y0 + y1), mz = 0.5 * (z0 + z1);
-                const uint32_t oct = (tcx >= mx ? 1u : 0u) | (tcy >= my ? 2u : 0u) | (tcz >= mz ? 4u : 0u);
-                const uint32_t lc = (uint32_t)(l - 1) << 27;
+                int cnt = 0;
 #pragma unroll
-                for (int c = 7; c >= 0; --c) {
-                    stack = (lane == sp) ? (int)(lc | ((code << 3) | (oct ^ (uint32_t)c))) : stack;
-                    ++sp;
+                for (int r = 0; r < 2 * kRowsPerLane; ++r) cnt += rc[r];
+                const int incl = wave_incl_scan_i(cnt);
+                const int off = incl - cnt;
+                const int total = __builtin_amdgcn_readlane(incl, 63);
+                // run table in LDS: entry lane*R+r = (first candidate index, first particle slot)
+#pragma unroll
+                for (int r = 0, pre = off; r < 2 * kRowsPerLane; ++r) {
+                    runs[lane * 2 * kRowsPerLane + r] = make_uint2((uint32_t)pre, rs[r]);
+                    pre += rc[r];
+                }
+                wave_lds_sync();
+                for (int cb = 0; cb < total; cb += kCap) {
+                    // ---- copy candidates [cb, cb + nc) into this wave's LDS buffer: lane i takes
+                    //      candidate cb + i + 64 t, finds its run by binary search in the run table
+                    //      (last entry with first index <= candidate), loads the record ----
+                    const int nc = min(kCap, total - cb);
+#pragma unroll
+                    for (int t = 0; t < kCap / 64; ++t) {
+                        const int i = cb + t * 64 + lane;
+                        if (t * 64 < nc && i < cb + nc) {
+                            int e = 0;
+#pragma unroll
+                            for (int stp = kRunEntries / 2; stp > 0; stp >>= 1)
+                                if ((int)runs[e + stp].x <= i) e += stp;
+                            const uint2 rn = runs[e];
+                            const uint32_t slot = rn.y + (uint32_t)(i - (int)rn.x);
+                            const double4 p4 = prec[slot];
+                            buf[i - cb] = make_double4(p4.x, p4.y, p4.z, __longlong_as_double((long long)slot));
+                        }
+                    }
+                    wave_lds_sync();
+                    // ---- every candidate against all 64 voxels ----
+                    for (int i = 0; i < nc; ++i) {
+                        const double4 c = buf[i];
+                        const double dx = qx - c.x, dy = qy - c.y, dz = qz - c.z;
+                        const double d2 = (dx * dx + dy * dy) + dz * dz;
+                        if (__builtin_amdgcn_ballot_w64(d2 < thr) != 0) {  // wave-uniform
+                            ++n_acc;
+                            insert<KMAX>(bd, bp, d2, (int)__double_as_longlong(c.w));  // no-op where d2 >= thr
+                            thr = fmin(bd[KMAX - 1], ub2);
+                        }
+                    }
+                    n_cand += (uint32_t)nc;
+                    wave_lds_sync();
                 }
             }
+            // ---- exactness: lanes with k-th distance <= R are final ----
+            const double worst = wave_max(bd[KMAX - 1]);  // inactive lanes hold -1
+            if (worst <= R * R || R >= a.rall) break;
+            Rp = R;
+            py0 = ry0;
+            py1 = ry1;
+            pz0 = rz0;
+            pz1 = rz1;
+            if (worst < INFINITY) {
+                R = sqrt(worst) * (1.0 + 1e-12);  // every list full: one exact pass left
+            } else if (R_ub < INFINITY && R < R_ub) {
+                R = R_ub;  // the coarse-lattice bound covers every lane
+            } else {
+                // some list not full.  Void tiles: grow geometrically while nothing has been
+                // found (rows only, no candidates), then in small steps so that the last
+                // shell does not overshoot the lens of particles the voxels actually need.
+                bool seen = false;
+#pragma unroll
+                for (int j = 0; j < KMAX; ++j) seen = seen || (bd[j] >= 0.0 && bd[j] < INFINITY);
+                const bool any_seen = __builtin_amdgcn_ballot_w64(seen) != 0;
+                R = any_seen ? R + fmax(a.r0, 0.125 * R) : 1.5 * R;
+            }
+            R = fmin(R, a.rall);
         }
     }
+    if (dbg != nullptr && lane == 0) {
+        atomicAdd(dbg + 0, 1ull);
+        atomicAdd(dbg + 1, (unsigned long long)n_pass);
+        atomicAdd(dbg + 2, (unsigned long long)n_round);
+        atomicAdd(dbg + 3, (unsigned long long)n_cand);
+        atomicAdd(dbg + 4, (unsigned long long)n_acc);
+    }
+    if (dbg != nullptr) atomicAdd(dbg + 5, (unsigned long long)n_rows);
 
     if (!valid) return;
     const size_t vo = ((size_t)(iz - a.z0) * a.ny + iy) * a.nx + ix;
+    if (a.mode == kModeKDist) {
+        U[vo] = sqrt(bd[KMAX - 1]);
+        return;
+    }
     if (!active) {
         U[vo] = 0.0;
         V[vo] = 0.0;
@@ -288,7 +474,7 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
     for (int c = 0; c < 3; ++c) {
         double t[KMAX];
 #pragma unroll
-        for (int j = 0; j < KMAX; ++j) t[j] = (j < k) ? w[j] * vb[(size_t)bp[j] * 4 + c] : 0.0;
+        for (int j = 0; j < KMAX; ++j) t[j] = (j < k) ? w[j] * vb[(size_t)max(bp[j], 0) * 4 + c] : 0.0;
         out[c] = pairwise<KMAX>(t, k);
     }
     if (a.flags & PTV_FLAG_NAN_TO_NUM) {
@@ -298,6 +484,17 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
     U[vo] = out[0];
     V[vo] = out[1];
     W[vo] = out[2];
+}
+
+__global__ void k_subsample(const double *__restrict__ in, int n, int step, double *__restrict__ out, int nout) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < nout) out[j] = in[min(j * step, n - 1)];
+}
+
+int launch_subsample(const double *in, int n, int step, double *out, int nout, hipStream_t s) {
+    hipLaunchKernelGGL(k_subsample, dim3((nout + 255) / 256), dim3(256), 0, s, in, n, step, out, nout);
+    PTV_HIP(hipGetLastError());
+    return PTV_OK;
 }
 
 static const int kKmaxList[] = {4, 8, 12, 16, 24, 32, 40, 48, 56, 64};
@@ -313,7 +510,7 @@ static void launch_t(dim3 grid, hipStream_t s, const KnnKernelArgs &ka, const Bi
                      const double *ay, const double *az, const double *qx, const double *qy, const double *qz,
                      const uint8_t *mask, double *U, double *V, double *W) {
     hipLaunchKernelGGL(k_knn_interp<KMAX>, grid, dim3(256), 0, s, ka, b.prec, b.pval, b.cstart, ax, ay, az, qx, qy,
-                       qz, mask, U, V, W);
+                       qz, mask, U, V, W, g_dbg);
 }
 
 int launch_knn(const KnnLaunch &a, const Binned &b, const double *ax, const double *ay, const double *az,
@@ -343,7 +540,19 @@ int launch_knn(const KnnLaunch &a, const Binned &b, const double *ax, const doub
     ka.power = a.power;
     ka.eps = a.eps;
     ka.flags = a.flags;
-    const long long nblocks = (long long)ka.ntxb * ka.nty * ka.ntz;
+    ka.r0 = a.r0;
+    ka.mode = a.mode;
+    ka.point_per_wave = a.point_per_wave;
+    ka.cb = a.cb;
+    double diag2 = 0.0;
+    for (int d = 0; d < 3; ++d) {
+        const double e = a.cg.cs[d] * a.cg.nc[d];
+        diag2 += e * e;
+    }
+    ka.rall = sqrt(diag2) * (1.0 + 1e-9) + a.cg.mg;
+    const long long nblocks = a.point_per_wave
+                                  ? ((long long)a.nx * a.ny * (a.z1 - a.z0) + 3) / 4
+                                  : (long long)ka.ntxb * ka.nty * ka.ntz;
     if (nblocks > 0x7fffffffLL) {
         set_error("grid too large for one launch");
         return PTV_E_ARG;

@@ -32,3 +32,21 @@ def normwise(a, b):
     den = np.max(np.abs(b[m]))
     num = np.max(np.abs(a[m] - b[m]))
     return num / den if den > 0 else num
+
+
+def boundary_ties(points, ax, ay, az, k):
+    """(nz, ny, nx) bool: voxels whose k-th and (k+1)-th nearest particles are equidistant.
+
+    At such voxels the neighbour SET depends on the search's tie order (cKDTree's is
+    traversal dependent), so no implementation can be held to the reference there.
+    """
+    from scipy.spatial import KDTree
+
+    Z, Y, X = np.meshgrid(az, ay, ax, indexing="ij")
+    q = np.stack([X.ravel(), Y.ravel(), Z.ravel()], -1)
+    kk = min(k + 1, len(points))
+    d, _ = KDTree(points).query(q, k=kk)
+    d = d.reshape(len(q), -1)
+    if kk <= k:
+        return np.zeros(X.shape, bool)
+    return (d[:, k - 1] == d[:, k]).reshape(X.shape)

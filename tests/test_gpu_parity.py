@@ -10,7 +10,7 @@ import numpy as np
 import pandas as pd
 import pytest
 
-from tests._util import load, names, normwise
+from tests._util import boundary_ties, load, names, normwise
 
 pytestmark = pytest.mark.gpu
 
@@ -41,8 +41,13 @@ def test_golden_parity(ctx, name):
     g = load(name)
     U, V, W = ctx.interp_knn(g["points"], g["values"], axes=(g["ax"], g["ay"], g["az"]), method=_method(g),
                              k=int(g["k"]), power=float(g["power"]))
+    keep = np.ones(U.shape, bool)
+    if int(g.get("tied", 0)):
+        # exclude voxels whose neighbour set is tie-order dependent (k-th == (k+1)-th distance)
+        keep = ~boundary_ties(g["points"], g["ax"], g["ay"], g["az"], int(g["k"]))
+        assert keep.mean() > 0.5
     for a, b in ((U, g["U"]), (V, g["V"]), (W, g["W"])):
-        assert normwise(a, b) <= TOL
+        assert normwise(a[keep], b[keep]) <= TOL
         if _exact(g):
             assert np.array_equal(a, b, equal_nan=True), f"not bit-exact: {np.sum(a != b)} voxels differ"
 
@@ -53,13 +58,14 @@ def test_masked_fused_epilogue(ctx):
 
     g = load("masked_spherepack_idw")
     axes = (g["ax"], g["ay"], g["az"])
+    keep = ~boundary_ties(g["points"], *axes, 8)  # boundary-particle lattice creates exact ties
     Ur, Vr, Wr = ctx.interp_knn(g["points"], g["values"], axes=axes, k=8, power=2.0)
     for a, b in ((Ur, g["U_raw"]), (Vr, g["V_raw"]), (Wr, g["W_raw"])):
-        assert normwise(a, b) <= TOL
+        assert normwise(a[keep], b[keep]) <= TOL
     U, V, W = ctx.interp_knn(g["points"], g["values"], axes=axes, k=8, power=2.0, fluid_mask=g["mask"],
                              flags=_lib.FLAG_NAN_TO_NUM)
     for a, b in ((U, g["U"]), (V, g["V"]), (W, g["W"])):
-        assert normwise(a, b) <= TOL
+        assert normwise(a[keep], b[keep]) <= TOL
     assert (U[~g["mask"]] == 0).all()
 
 
