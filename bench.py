@@ -1,0 +1,244 @@
+#!/usr/bin/env python3
+"""Headline benchmark: k-NN IDW of 5M sphere-pack particles onto a 512^3 grid (fp64).
+
+Metric (BASELINE.json): Mvoxels/s interpolated + achieved HBM GB/s, 512^3 grid /
+5M particles IDW.  One *step* = one full pass of the hot path with every input
+already resident in HBM: bounding box + particle binning + coarse-lattice bounds +
+the k-NN IDW kernel writing U, V, W (the reference rebuilds its KDTree on every
+call, interpolator.py:132, so the binning is inside the step).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
+
+Multi-GPU (weak scaling): rank r owns z-slab copy r of a stack of
+sphere packs along z (grid 512 x 512 x 512N, 5M particles per copy); it bins its
+own copy plus the particles of the neighbouring copies within `--halo` voxels of
+its slab and interpolates its 512^3 slab.  No collective touches the data path;
+the barrier + max-over-ranks timing uses torch.distributed (RCCL).
+`value` = all voxels of all ranks / max rank time.
+
+Rank 0 prints ONE JSON line.  `roofline.achieved` = algorithmic bytes of the k-NN
+kernel, V*(6k+3)*8 (SURVEY.md §8(d) gather model), / its hipEvent-timed average
+duration.  `roofline.traffic` is read from profiles/traffic_*.json (rocprofv3
+FETCH_SIZE/WRITE_SIZE passes, tools/collect_traffic.sh) when present.
+`cpu_baseline` times the oracle restatement of interpolator.py:126-155
+(scipy KDTree + numpy) over z-slabs on a ProcessPoolExecutor — the
+interpolator.py:173-182 / test_parallel.py multiprocess pattern — on a bounded
+sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Mvoxels/s interpolated + achieved HBM GB/s, 512³ grid / 5M particles IDW"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--grid", type=int, default=512)
+    ap.add_argument("--particles", type=int, default=5_000_000)
+    ap.add_argument("--k", type=int, default=8)
+    ap.add_argument("--power", type=float, default=2.0)
+    ap.add_argument("--method", default="idw", choices=["idw", "sibson"])
+    ap.add_argument("--halo", type=int, default=64, help="neighbour-copy halo (voxels) for N>1")
+    ap.add_argument("--cpu-sample-planes", type=int, default=16)
+    ap.add_argument("--cpu-workers", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--allgather", action="store_true", help="also time an RCCL all-gather of U,V,W (reported apart)")
+    return ap.parse_args()
+
+
+def rank_particles(args, rank, world, values="reference"):
+    """Particles of pack copy `rank` plus halo particles of copies rank+-1 (weak scaling)."""
+    from ptv_interpolation_amd import synth
+
+    G = args.grid
+    P, Q = synth.sphere_pack(args.particles, G, values=values, z_tiles=world, z_tile=rank)
+    if world == 1:
+        return P, Q
+    parts, vals = [P], [Q]
+    z_lo, z_hi = rank * G, (rank + 1) * G
+    for nb in (rank - 1, rank + 1):
+        if 0 <= nb < world:
+            Pn, Qn = synth.sphere_pack(args.particles, G, values=values, z_tiles=world, z_tile=nb)
+            keep = (Pn[:, 2] >= z_lo - args.halo) & (Pn[:, 2] < z_hi + args.halo)
+            parts.append(Pn[keep])
+            vals.append(Qn[keep])
+    return np.concatenate(parts), np.concatenate(vals)
+
+
+def traffic_from_profiles(kernel_substr="k_knn_interp<"):
+    """HBM bytes per k-NN launch from the newest profiles/traffic_*.json (or None)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "traffic_*.json")))
+    if not files:
+        return None
+    try:
+        with open(files[-1]) as f:
+            t = json.load(f)
+        return float(t["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def cpu_baseline(args, P, Q, ax):
+    """Oracle restatement on a bounded z-slab sample, multiprocess (test_parallel.py pattern)."""
+    from oracle import cpu_ref
+
+    planes = min(args.cpu_sample_planes, len(ax))
+    z0 = len(ax) // 2 - planes // 2
+    workers = max(1, min(args.cpu_workers, os.cpu_count() or 1))
+    t = time.perf_counter()
+    cpu_ref.interp_grid_parallel(P, Q, ax, ax, ax, args.method, args.k, args.power,
+                                 z0=z0, z1=z0 + planes, n_jobs=workers, slab=max(1, planes // workers))
+    dt = time.perf_counter() - t
+    nvox = planes * len(ax) * len(ax)
+    return {"value": round(nvox / dt / 1e6, 4), "unit": "Mvoxels/s", "cores": workers, "kind": "port",
+            "sample": f"{planes} central z-planes ({nvox} voxels) of the same {args.grid}^3/"
+                      f"{args.particles} workload; scipy KDTree + numpy (oracle/cpu_ref.py), "
+                      f"{workers} processes, each building its own tree (interpolator.py:173-182 pattern)",
+            "seconds": round(dt, 2)}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from ptv_interpolation_amd import _lib
+
+    G = args.grid
+    P, Q = rank_particles(args, rank, world)
+    n = P.shape[0]
+    ax_h = np.linspace(0, G - 1, G)
+    az_h = ax_h + rank * G
+    cols = [torch.from_numpy(np.ascontiguousarray(P[:, i])).to(dev) for i in range(3)] + \
+           [torch.from_numpy(np.ascontiguousarray(Q[:, i])).to(dev) for i in range(3)]
+    axes = [torch.from_numpy(ax_h).to(dev), torch.from_numpy(ax_h.copy()).to(dev), torch.from_numpy(az_h).to(dev)]
+    out = [torch.empty((G, G, G), dtype=torch.float64, device=dev) for _ in range(3)]
+    ctx = _lib.Context(local)
+    method = _lib.METHOD_IDW if args.method == "idw" else _lib.METHOD_SIBSON
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        return ctx.interp_knn_dev(n, [c.data_ptr() for c in cols], G, G, G,
+                                  axes_ptrs=[a.data_ptr() for a in axes],
+                                  out_ptrs=[o.data_ptr() for o in out], method=method, k=args.k,
+                                  power=args.power, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    knn_ms, lat_ms, bin_ms = [], [], []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        st = ctx.last_stats()  # synchronises on the step's events
+        knn_ms.append(st["ms_knn"])
+        lat_ms.append(st["ms_lattice"])
+        bin_ms.append(st["ms_bin"])
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    gather_ms = None
+    if args.allgather and dist is not None:
+        full = [torch.empty((G * world, G, G), dtype=torch.float64, device=dev) for _ in range(3)]
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        tg = time.perf_counter()
+        for c in range(3):
+            dist.all_gather_into_tensor(full[c], out[c])
+        torch.cuda.synchronize(dev)
+        gather_ms = (time.perf_counter() - tg) * 1e3
+        del full
+
+    vox = G ** 3
+    ms_step = elapsed / args.steps * 1e3
+    value = vox * world / (elapsed / args.steps) / 1e6
+    knn_avg = float(np.mean(knn_ms))
+    alg_bytes = vox * (6 * args.k + 3) * 8
+    achieved = alg_bytes / (knn_avg * 1e-3) / 1e9
+    traffic = traffic_from_profiles()
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(args, P, Q, ax_h)
+        except Exception as e:  # the baseline must never take the GPU line down
+            cpu = {"value": None, "error": repr(e)[:200]}
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "Mvoxels/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: generate_sphere_pack.py geometry scaled to voxel units, seeded, w=1 flow field",
+            "config": {"workload": f"{G}^3 grid / {args.particles} particles {args.method.upper()} "
+                                   f"k={args.k} p={args.power} fp64 (z-slab per GPU)",
+                       "grid": G, "particles": args.particles, "particles_binned_rank0": n,
+                       "method": args.method, "k": args.k, "power": args.power,
+                       "parallelism": f"z-slab x{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                         "traffic": traffic, "kernel": "k_knn_interp<8>",
+                         "alg_bytes_per_launch": alg_bytes, "kernel_ms": round(knn_avg, 3)},
+            "cpu_baseline": cpu,
+            "breakdown_ms": {"bin": round(float(np.mean(bin_ms)), 3), "lattice": round(float(np.mean(lat_ms)), 3),
+                             "knn": round(knn_avg, 3)},
+        }
+        if gather_ms is not None:
+            line["allgather_ms"] = round(gather_ms, 2)
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -102,6 +102,8 @@ typedef struct {
 
 /* Library / device management. */
 int ptv_version(void);
+/* sizeof(ptv_particles, ptv_grid, ptv_knn_params, ptv_stats): binding self-check */
+int ptv_abi_sizes(int64_t out4[4]);
 const char *ptv_last_error(void);
 int ptv_device_count(int *out);
 int ptv_init(int device, ptv_ctx **out);

@@ -65,6 +65,7 @@ class Stats(C.Structure):
 
 EXPORTS = {
     "ptv_version": (C.c_int, []),
+    "ptv_abi_sizes": (C.c_int, [C.POINTER(C.c_int64)]),
     "ptv_last_error": (C.c_char_p, []),
     "ptv_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "ptv_init": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
@@ -117,6 +118,14 @@ def check(rc):
             raise NotImplementedError(msg)
         raise PtvError(rc, msg)
     return rc
+
+
+def abi_sizes():
+    """(C sizeof, ctypes sizeof) for each ABI struct: they must agree."""
+    out = (C.c_int64 * 4)()
+    check(lib().ptv_abi_sizes(out))
+    py = [C.sizeof(Particles), C.sizeof(Grid), C.sizeof(KnnParams), C.sizeof(Stats)]
+    return list(out), py
 
 
 def device_count() -> int:

@@ -78,6 +78,18 @@ extern "C" {
 
 int ptv_version(void) { return PTV_API_VERSION; }
 
+int ptv_abi_sizes(int64_t out4[4]) {
+    if (!out4) {
+        set_error("ptv_abi_sizes: out is NULL");
+        return PTV_E_ARG;
+    }
+    out4[0] = (int64_t)sizeof(ptv_particles);
+    out4[1] = (int64_t)sizeof(ptv_grid);
+    out4[2] = (int64_t)sizeof(ptv_knn_params);
+    out4[3] = (int64_t)sizeof(ptv_stats);
+    return PTV_OK;
+}
+
 const char *ptv_last_error(void) { return g_last_error.c_str(); }
 
 int ptv_device_count(int *out) {

@@ -1,0 +1,101 @@
+"""Host-side logic of the drop-in module (no GPU): grid construction and
+introspection, argument validation mirroring the reference's exceptions,
+I/O helpers, mask resampling and boundary particles vs the reference's outputs."""
+import numpy as np
+import pandas as pd
+import pytest
+
+from ptv_interpolation_amd import interpolator as ip
+from ptv_interpolation_amd import synth
+from tests._util import load
+
+
+def test_create_grid_matches_reference_axes():
+    g = load("idw_aniso_k13")
+    (X, Y, Z), (x, y, z) = ip.create_grid(((-3.2, 5.1), (10.0, 14.0), (0.5, 2.0)), (20, 12, 9))
+    assert np.array_equal(x, g["ax"]) and np.array_equal(y, g["ay"]) and np.array_equal(z, g["az"])
+    assert X.shape == (9, 12, 20)
+    assert np.array_equal(X[3, 4, :], x) and np.array_equal(Y[2, :, 5], y) and np.array_equal(Z[:, 1, 1], z)
+
+
+def test_create_grid_views_equal_dense():
+    (Xd, Yd, Zd), _ = ip.create_grid(((0, 7), (1, 9), (2, 6)), (7, 8, 4))
+    (Xv, Yv, Zv), _ = ip.create_grid(((0, 7), (1, 9), (2, 6)), (7, 8, 4), dense=False)
+    for a, b in ((Xd, Xv), (Yd, Yv), (Zd, Zv)):
+        assert a.shape == b.shape and np.array_equal(a, b)
+
+
+def test_separable_axes_detection():
+    (X, Y, Z), (x, y, z) = ip.create_grid(((0, 10), (0, 6), (0, 4)), (10, 6, 4))
+    ax, ay, az = ip.separable_axes(X, Y, Z)
+    assert np.array_equal(ax, x) and np.array_equal(ay, y) and np.array_equal(az, z)
+    (Xv, Yv, Zv), _ = ip.create_grid(((0, 10), (0, 6), (0, 4)), (10, 6, 4), dense=False)
+    assert ip.separable_axes(Xv, Yv, Zv) is not None
+    X2 = X.copy(); X2[1, 2, 3] += 0.5
+    assert ip.separable_axes(X2, Y, Z) is None
+    assert ip.separable_axes(X.ravel(), Y.ravel(), Z.ravel()) is None
+
+
+def _df(n=20, seed=0):
+    r = np.random.default_rng(seed)
+    P = r.uniform(0, 5, (n, 3)); Q = r.standard_normal((n, 3))
+    return pd.DataFrame({"x": P[:, 0], "y": P[:, 1], "z": P[:, 2], "u": Q[:, 0], "v": Q[:, 1], "w": Q[:, 2]})
+
+
+def test_reference_exceptions_before_any_gpu_call(capsys):
+    """k=1 -> AxisError, k>N -> IndexError, as the reference raises (interpolator.py:139-153)."""
+    grid, _ = ip.create_grid(((0, 4),) * 3, 4)
+    df = _df(10)
+    with pytest.raises(np.exceptions.AxisError):
+        ip.interpolate_field(df, grid, method="idw", idw_neighbors=1)
+    with pytest.raises(IndexError):
+        ip.interpolate_field(df, grid, method="idw", idw_neighbors=11)
+    with pytest.raises(np.exceptions.AxisError):
+        ip.interpolate_field(df, grid, method="sibson", sibson_neighbors=1)
+    out = capsys.readouterr().out
+    assert "Using IDW Interpolation (power=2.0, neighbors=1)..." in out
+    assert "Using Sibson (Natural Neighbor) Interpolation (neighbors=1)..." in out
+
+
+def test_griddata_methods_pass_through():
+    """linear/nearest stay scipy griddata (interpolator.py:196-197, outside the accelerated path)."""
+    grid, _ = ip.create_grid(((0, 4),) * 3, 4)
+    U, V, W = ip.interpolate_field(_df(60), grid, method="nearest")
+    assert U.shape == (4, 4, 4) and np.isfinite(U).all()
+
+
+def test_load_ptv_data_renames(tmp_path):
+    p = tmp_path / "p.csv"
+    pd.DataFrame({"x": [0.0, 1.0], "y": [0.0, 1.0], "z": [0.0, 1.0], "vx": [1.0, 2.0], "vy": [0.0, 0.0],
+                  "vz": [3.0, 4.0]}).to_csv(p, index=False)
+    df = ip.load_ptv_data(str(p))
+    assert list(df["u"]) == [1.0, 2.0] and list(df["w"]) == [3.0, 4.0]
+    bad = tmp_path / "b.csv"
+    pd.DataFrame({"x": [0.0]}).to_csv(bad, index=False)
+    with pytest.raises(IOError):
+        ip.load_ptv_data(str(bad))
+
+
+def test_mask_sampling_and_boundary_particles_match_reference():
+    g = load("masked_spherepack_idw")
+    fluid = g["fluid_raw"]
+    G = fluid.shape[0]
+    bounds = ((0, G),) * 3
+    (X, Y, Z), _ = ip.create_grid(bounds, (32, 32, 32))
+    assert np.array_equal(ip.sample_mask_on_grid(fluid, (X, Y, Z), bounds), g["mask"])
+    bx, by, bz = ip.extract_boundary_particles(fluid, bounds, sampling_step=3, thickness=1)
+    nb = len(bx)
+    P = g["points"]
+    assert np.array_equal(P[-nb:, 0], bx) and np.array_equal(P[-nb:, 1], by) and np.array_equal(P[-nb:, 2], bz)
+
+
+def test_sphere_pack_is_seeded_and_exact_count():
+    P1, Q1 = synth.sphere_pack(5000, 40)
+    P2, Q2 = synth.sphere_pack(5000, 40)
+    assert P1.shape == (5000, 3) and np.array_equal(P1, P2)
+    assert (P1 >= 0).all() and (P1 <= 39).all()
+    assert (Q1[:, 2] == 1.0).all() and (Q1[:, :2] == 0.0).all()
+    # no particle inside a sphere (generate_sphere_pack.py:50-54, :95-97)
+    lo, hi = synth.LO, synth.HI
+    D = lo + P1 / 39.0 * (hi - lo)
+    assert not synth.inside_spheres(D[:, 0], D[:, 1], D[:, 2]).any()
