@@ -384,6 +384,12 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
     Binned b{c->prec.p, c->pval.p, c->start.p, n};
     PTV_HIP(hipEventRecord(c->ev_knn0, s));
     for (int l = nlat - 1; l >= 0; --l) {  // coarsest first
+        if (l == nlat - 1) {
+            // coarsest lattice: count-only upper bounds (no candidate is read)
+            PTV_TRY(launch_count_bound(cg, c->start.p, lat[l].ax, lat[l].ay, lat[l].az, lat[l].n[0], lat[l].n[1],
+                                       lat[l].n[2], prm->k, kl.r0, lat[l].dk, s));
+            continue;
+        }
         KnnLaunch ll = kl;
         ll.nx = lat[l].n[0];
         ll.ny = lat[l].n[1];
@@ -392,15 +398,12 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
         ll.z1 = lat[l].n[2];
         ll.mode = kModeKDist;
         ll.flags = 0;
-        ll.point_per_wave = (l == nlat - 1) ? 1 : 0;
-        if (l + 1 < nlat) {
-            ll.cb.ax = lat[l + 1].ax;
-            ll.cb.ay = lat[l + 1].ay;
-            ll.cb.az = lat[l + 1].az;
-            ll.cb.dk = lat[l + 1].dk;
-            for (int d = 0; d < 3; ++d) ll.cb.n[d] = lat[l + 1].n[d];
-            ll.cb.step = kLatticeStep;
-        }
+        ll.cb.ax = lat[l + 1].ax;
+        ll.cb.ay = lat[l + 1].ay;
+        ll.cb.az = lat[l + 1].az;
+        ll.cb.dk = lat[l + 1].dk;
+        for (int d = 0; d < 3; ++d) ll.cb.n[d] = lat[l + 1].n[d];
+        ll.cb.step = kLatticeStep;
         PTV_TRY(launch_knn(ll, b, lat[l].ax, lat[l].ay, lat[l].az, nullptr, nullptr, nullptr, nullptr, lat[l].dk,
                            lat[l].dk, lat[l].dk, s));
     }

@@ -49,6 +49,11 @@ struct KnnLaunch {
     CoarseBound cb;
 };
 
+// Upper bound on the k-th neighbour distance of every point of a separable grid by
+// counting the particles of cells entirely inside balls around it (coarsest lattice).
+int launch_count_bound(const CellGrid &g, const uint32_t *cstart, const double *ax, const double *ay,
+                       const double *az, int nx, int ny, int nz, int k, double r0, double *out, hipStream_t s);
+
 // out[j] = in[min(step*j, n-1)] for j < nout (lattice axes)
 int launch_subsample(const double *in, int n, int step, double *out, int nout, hipStream_t s);
 

@@ -113,6 +113,14 @@ __device__ __forceinline__ double nan_to_num(double v) {
     return v;
 }
 
+// a wave-uniform double held in SGPRs
+__device__ __forceinline__ double uniform(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffffLL));
+    const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
 __device__ __forceinline__ double wave_min(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
@@ -147,23 +155,31 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 template <int KMAX>
 __device__ __forceinline__ void insert(double (&bd)[KMAX], int (&bp)[KMAX], double d2, int p) {
-    // descending sweep: slot j takes slot j-1 if the candidate beats j-1, else the
-    // candidate if it beats j, else keeps its value (two live compare masks only)
-    bool lt_j = d2 < bd[KMAX - 1];
+    // Descending sweep: slot j takes slot j-1 if the candidate beats j-1, else the candidate
+    // if it beats j, else keeps its value.  Written as bit-selects on all-ones/all-zeros
+    // masks so the compiler emits v_cmp + v_cndmask (no exec-mask branches).
+    const unsigned long long cu = (unsigned long long)__double_as_longlong(d2);
+    unsigned long long m_j = 0ull - (unsigned long long)(d2 < bd[KMAX - 1]);
 #pragma unroll
     for (int j = KMAX - 1; j > 0; --j) {
-        const bool lt_m = d2 < bd[j - 1];
-        const double nd = lt_m ? bd[j - 1] : (lt_j ? d2 : bd[j]);
-        const int np = lt_m ? bp[j - 1] : (lt_j ? p : bp[j]);
-        bd[j] = nd;
-        bp[j] = np;
-        lt_j = lt_m;
+        const unsigned long long m_m = 0ull - (unsigned long long)(d2 < bd[j - 1]);
+        const unsigned long long cur = (unsigned long long)__double_as_longlong(bd[j]);
+        const unsigned long long prv = (unsigned long long)__double_as_longlong(bd[j - 1]);
+        unsigned long long t = (cur & ~m_j) | (cu & m_j);
+        t = (t & ~m_m) | (prv & m_m);
+        int ti = (bp[j] & ~(int)m_j) | (p & (int)m_j);
+        ti = (ti & ~(int)m_m) | (bp[j - 1] & (int)m_m);
+        bd[j] = __longlong_as_double((long long)t);
+        bp[j] = ti;
+        m_j = m_m;
     }
-    if (lt_j) {
-        bd[0] = d2;
-        bp[0] = p;
-    }
+    const unsigned long long cur0 = (unsigned long long)__double_as_longlong(bd[0]);
+    bd[0] = __longlong_as_double((long long)((cur0 & ~m_j) | (cu & m_j)));
+    bp[0] = (bp[0] & ~(int)m_j) | (p & (int)m_j);
 }
+
+// min(a, b) for non-NaN operands without fmin's canonicalising v_max
+__device__ __forceinline__ double dmin(double a, double b) { return a < b ? a : b; }
 
 __device__ __forceinline__ int clampi(double f, int n) {
     return f < 0.0 ? 0 : (f >= (double)(n - 1) ? n - 1 : (int)f);
@@ -257,18 +273,18 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
         bd[j] = (!active || j < a.kpad) ? -1.0 : INFINITY;
         bp[j] = -1;
     }
-    double thr = fmin(bd[KMAX - 1], ub2);
+    double thr = dmin(bd[KMAX - 1], ub2);
     uint32_t n_pass = 0, n_round = 0, n_rows = 0, n_cand = 0, n_acc = 0;
 
     if (__builtin_amdgcn_ballot_w64(active) != 0) {
-        const double bx0 = wave_min(active ? qx : INFINITY), bx1 = wave_max(active ? qx : -INFINITY);
-        const double by0 = wave_min(active ? qy : INFINITY), by1 = wave_max(active ? qy : -INFINITY);
-        const double bz0 = wave_min(active ? qz : INFINITY), bz1 = wave_max(active ? qz : -INFINITY);
+        const double bx0 = uniform(wave_min(active ? qx : INFINITY)), bx1 = uniform(wave_max(active ? qx : -INFINITY));
+        const double by0 = uniform(wave_min(active ? qy : INFINITY)), by1 = uniform(wave_max(active ? qy : -INFINITY));
+        const double bz0 = uniform(wave_min(active ? qz : INFINITY)), bz1 = uniform(wave_max(active ? qz : -INFINITY));
         const CellGrid &g = a.cg;
         double Rp = -1.0;  // radius already gathered (none yet)
         // R_ub covers every lane's k-th neighbour: small (fluid) -> try r0 first and then
         // the exact max k-th distance; large (void) -> one pass at R_ub.
-        const double R_ub = wave_max(active ? ub : -INFINITY);
+        const double R_ub = uniform(wave_max(active ? ub : -INFINITY));
         double R = a.r0;
         if (R_ub < INFINITY) R = fmin(R_ub, a.r0);
         int py0 = 1, py1 = 0, pz0 = 1, pz1 = 0;  // row box of the previous pass (empty)
@@ -365,7 +381,7 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
                         if (__builtin_amdgcn_ballot_w64(d2 < thr) != 0) {  // wave-uniform
                             ++n_acc;
                             insert<KMAX>(bd, bp, d2, (int)__double_as_longlong(c.w));  // no-op where d2 >= thr
-                            thr = fmin(bd[KMAX - 1], ub2);
+                            thr = dmin(bd[KMAX - 1], ub2);
                         }
                     }
                     n_cand += (uint32_t)nc;
@@ -373,7 +389,7 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
                 }
             }
             // ---- exactness: lanes with k-th distance <= R are final ----
-            const double worst = wave_max(bd[KMAX - 1]);  // inactive lanes hold -1
+            const double worst = uniform(wave_max(bd[KMAX - 1]));  // inactive lanes hold -1
             if (worst <= R * R || R >= a.rall) break;
             Rp = R;
             py0 = ry0;
@@ -484,6 +500,89 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
     U[vo] = out[0];
     V[vo] = out[1];
     W[vo] = out[2];
+}
+
+// ---------------------------------------------------------------------------
+// Count-only k-th distance UPPER bound (coarsest lattice).  One wave per grid point;
+// the lanes share the cell rows of a ball of radius R around it and count only the
+// particles of cells lying entirely inside the ball (at most the particles within R),
+// so count(R) >= k proves d_k <= R.  R grows by 1.5x until that holds, then a
+// bisection tightens it.  No particle record is read.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int count_inside(const CellGrid &g, const uint32_t *__restrict__ cstart, double qx,
+                                            double qy, double qz, double R, int lane) {
+    const double Ri = R - g.mg;  // conservative: shrink by the binning margin
+    if (Ri <= 0.0) return 0;
+    const double R2 = Ri * Ri;
+    const int ry0 = clampi(floor((qy - Ri - g.o[1]) * g.ic[1]), g.nc[1]);
+    const int ry1 = clampi(floor((qy + Ri - g.o[1]) * g.ic[1]), g.nc[1]);
+    const int rz0 = clampi(floor((qz - Ri - g.o[2]) * g.ic[2]), g.nc[2]);
+    const int rz1 = clampi(floor((qz + Ri - g.o[2]) * g.ic[2]), g.nc[2]);
+    const int nyr = ry1 - ry0 + 1;
+    const int nrows = nyr * (rz1 - rz0 + 1);
+    int cnt = 0;
+    for (int row = lane; row < nrows; row += 64) {
+        const int ccy = ry0 + row % nyr, ccz = rz0 + row / nyr;
+        const double y0 = g.o[1] + (double)ccy * g.cs[1], y1 = g.o[1] + (double)(ccy + 1) * g.cs[1];
+        const double z0 = g.o[2] + (double)ccz * g.cs[2], z1 = g.o[2] + (double)(ccz + 1) * g.cs[2];
+        const double fy = fmax(fabs(y0 - qy), fabs(y1 - qy)), fz = fmax(fabs(z0 - qz), fabs(z1 - qz));
+        const double h2 = fy * fy + fz * fz;
+        if (h2 >= R2) continue;
+        const double rx = sqrt(R2 - h2) * (1.0 - 1e-12);
+        // cells [a, b] whose x-extent lies inside [qx - rx, qx + rx]
+        const int a = (int)ceil((qx - rx - g.o[0]) * g.ic[0] + 1e-9);
+        const int b = (int)floor((qx + rx - g.o[0]) * g.ic[0] - 1e-9) - 1;
+        const int aa = max(a, 0), bb = min(b, g.nc[0] - 1);
+        if (aa > bb) continue;
+        const long long base = ((long long)ccz * g.nc[1] + ccy) * g.nc[0];
+        cnt += (int)(cstart[base + bb + 1] - cstart[base + aa]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+    return cnt;
+}
+
+__global__ __launch_bounds__(256) void k_count_bound(CellGrid g, const uint32_t *__restrict__ cstart,
+                                                     const double *__restrict__ ax, const double *__restrict__ ay,
+                                                     const double *__restrict__ az, int nx, int ny, int nz, int k,
+                                                     double r0, double rall, double *__restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const long long gp = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (gp >= (long long)nx * ny * nz) return;  // wave-uniform
+    const int ix = (int)(gp % nx), iy = (int)((gp / nx) % ny), iz = (int)(gp / ((long long)nx * ny));
+    const double qx = ax[ix], qy = ay[iy], qz = az[iz];
+    double lo = 0.0, hi = r0;
+    while (hi < rall && count_inside(g, cstart, qx, qy, qz, hi, lane) < k) {
+        lo = hi;
+        hi *= 1.5;
+    }
+    if (hi >= rall) {
+        hi = rall;
+    } else {
+        for (int it = 0; it < 6; ++it) {
+            const double mid = 0.5 * (lo + hi);
+            if (count_inside(g, cstart, qx, qy, qz, mid, lane) >= k)
+                hi = mid;
+            else
+                lo = mid;
+        }
+    }
+    if (lane == 0) out[gp] = hi * (1.0 + 1e-12) + g.mg;
+}
+
+int launch_count_bound(const CellGrid &g, const uint32_t *cstart, const double *ax, const double *ay,
+                       const double *az, int nx, int ny, int nz, int k, double r0, double *out, hipStream_t s) {
+    double diag2 = 0.0;
+    for (int d = 0; d < 3; ++d) {
+        const double e = g.cs[d] * g.nc[d];
+        diag2 += e * e;
+    }
+    const double rall = sqrt(diag2) * (1.0 + 1e-9) + g.mg;
+    const long long pts = (long long)nx * ny * nz;
+    hipLaunchKernelGGL(k_count_bound, dim3((unsigned)((pts + 3) / 4)), dim3(256), 0, s, g, cstart, ax, ay, az, nx, ny,
+                       nz, k, r0, rall, out);
+    PTV_HIP(hipGetLastError());
+    return PTV_OK;
 }
 
 __global__ void k_subsample(const double *__restrict__ in, int n, int step, double *__restrict__ out, int nout) {
