@@ -137,12 +137,13 @@ int ptv_interp_knn_dev(ptv_ctx *ctx, const ptv_particles *p, const ptv_grid *g,
 int ptv_last_stats(ptv_ctx *ctx, ptv_stats *st);
 
 /*
- * Diagnostics: mode 1 = enable + zero the k-NN traversal counters, 0 = disable,
- * other = leave as is.  If out6 != NULL the (synchronised) totals are copied:
- * {waves, nodes popped, nodes visited, leaves scanned, candidates, candidates
- * accepted by at least one lane}.  Not thread-safe; for profiling only.
+ * Diagnostics: mode 1 = enable + zero per-wave phase stamps of the k-NN kernel (k <= 8
+ * launches switch to an s_memtime-stamped build), 0 = disable, other = leave.  If out
+ * != NULL (19 doubles) it receives {waves recorded, mean[9], max[9]} over the fields
+ * {setup, rows, copy, compute, epilogue cycles, candidates, accepted, rounds, passes}.
+ * Profiling only: stamps perturb the schedule; never time a stamped run.
  */
-int ptv_debug_counters(ptv_ctx *ctx, int mode, unsigned long long *out6);
+int ptv_debug_stamps(ptv_ctx *ctx, int mode, double *out19);
 
 #ifdef __cplusplus
 }

@@ -75,7 +75,7 @@ EXPORTS = {
     "ptv_interp_knn_dev": (C.c_int, [C.c_void_p, C.POINTER(Particles), C.POINTER(Grid), C.POINTER(KnnParams),
                                      _dp, _dp, _dp, C.c_void_p, C.POINTER(Stats)]),
     "ptv_last_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
-    "ptv_debug_counters": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_uint64)]),
+    "ptv_debug_stamps": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_double)]),
 }
 
 _lib = None
@@ -174,12 +174,13 @@ class Context:
         check(lib().ptv_last_stats(self.h, C.byref(st)))
         return st.as_dict()
 
-    def debug_counters(self, mode=2):
-        """mode 1: enable+zero, 0: disable, 2: read. Returns the six traversal totals."""
-        out = (C.c_uint64 * 6)()
-        check(lib().ptv_debug_counters(self.h, int(mode), out))
-        keys = ("waves", "passes", "rounds", "candidates", "accepted", "rows")
-        return dict(zip(keys, list(out)))
+    def debug_stamps(self, mode=2):
+        """mode 1: enable+zero, 0: disable, 2: read.  Per-wave phase cycles (mean / max)."""
+        out = (C.c_double * 19)()
+        check(lib().ptv_debug_stamps(self.h, int(mode), out))
+        keys = ("setup", "rows", "copy", "compute", "epilogue", "candidates", "accepted", "rounds", "passes")
+        v = list(out)
+        return {"waves": v[0], "mean": dict(zip(keys, v[1:10])), "max": dict(zip(keys, v[10:19]))}
 
     # -- host buffers ------------------------------------------------------
     def interp_knn(self, points, values, axes=None, grid_points=None, shape=None, method=METHOD_IDW, k=8,

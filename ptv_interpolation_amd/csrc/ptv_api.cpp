@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/ptv_api.h"
 #include "ptv_kernels.hpp"
@@ -556,23 +557,49 @@ int ptv_interp_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const 
     return PTV_OK;
 }
 
-int ptv_debug_counters(ptv_ctx *c, int mode, unsigned long long *out6) {
+int ptv_debug_stamps(ptv_ctx *c, int mode, double *out) {
     if (!c) {
         set_error("NULL context");
         return PTV_E_ARG;
     }
     PTV_HIP(hipSetDevice(c->device));
+    constexpr long long cap = 1LL << 21;  // waves recorded (modulo-free: later waves dropped)
+    constexpr int nf = 8;
     if (mode == 1) {  // enable + zero
-        PTV_TRY(c->dbg.ensure(8));
-        PTV_HIP(hipMemsetAsync(c->dbg.p, 0, 8 * sizeof(unsigned long long), c->stream));
+        PTV_TRY(c->dbg.ensure((size_t)cap * nf));
+        PTV_HIP(hipMemsetAsync(c->dbg.p, 0, (size_t)cap * nf * sizeof(unsigned long long), c->stream));
         PTV_HIP(hipStreamSynchronize(c->stream));
         ptv::g_dbg = c->dbg.p;
+        ptv::g_dbg_cap = cap;
     } else if (mode == 0) {
         ptv::g_dbg = nullptr;
+        ptv::g_dbg_cap = 0;
     }
-    if (out6 && c->dbg.p) {
+    if (out && c->dbg.p) {
         PTV_HIP(hipDeviceSynchronize());
-        PTV_HIP(hipMemcpy(out6, c->dbg.p, 6 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        std::vector<unsigned long long> h((size_t)cap * nf);
+        PTV_HIP(hipMemcpy(h.data(), c->dbg.p, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        // out: [records, mean of 9 fields, max of 9 fields] (field 7 split into rounds, passes)
+        double sum[9] = {0}, mx[9] = {0};
+        long long nrec = 0;
+        for (long long w = 0; w < cap; ++w) {
+            const unsigned long long *r = &h[(size_t)w * nf];
+            if (r[0] == 0 && r[1] == 0 && r[4] == 0) continue;
+            ++nrec;
+            double v[9];
+            for (int f = 0; f < 7; ++f) v[f] = (double)r[f];
+            v[7] = (double)(r[7] & 0xffffffffULL);
+            v[8] = (double)(r[7] >> 32);
+            for (int f = 0; f < 9; ++f) {
+                sum[f] += v[f];
+                mx[f] = std::max(mx[f], v[f]);
+            }
+        }
+        out[0] = (double)nrec;
+        for (int f = 0; f < 9; ++f) {
+            out[1 + f] = nrec ? sum[f] / (double)nrec : 0.0;
+            out[10 + f] = mx[f];
+        }
     }
     return PTV_OK;
 }

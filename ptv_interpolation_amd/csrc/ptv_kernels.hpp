@@ -58,7 +58,8 @@ int launch_count_bound(const CellGrid &g, const uint32_t *cstart, const double *
 int launch_subsample(const double *in, int n, int step, double *out, int nout, hipStream_t s);
 
 int kmax_for(int k);  // compile-time list length serving k, 0 if unsupported
-extern unsigned long long *g_dbg;  // traversal counters (diagnostics), NULL = off
+extern unsigned long long *g_dbg;  // per-wave phase stamps (diagnostics), NULL = off
+extern long long g_dbg_cap;
 
 int launch_knn(const KnnLaunch &a, const Binned &b, const double *ax, const double *ay, const double *az,
                const double *qx, const double *qy, const double *qz, const uint8_t *mask, double *U, double *V,

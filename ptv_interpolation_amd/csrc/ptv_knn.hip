@@ -41,12 +41,15 @@
 
 namespace ptv {
 
-constexpr int kCap = 256;        // LDS candidate slots per wave (32 B each)
+constexpr int kStampFields = 8;
+constexpr int kCap = 128;        // LDS candidate slots per wave (16 B fp32 + 32 B fp64 each)
 constexpr int kRowsPerLane = 2;  // cell rows examined per lane per gather round
 constexpr int kRunEntries = 64 * 2 * kRowsPerLane;  // x-runs per gather round (power of two)
 
-// optional per-launch search counters (device buffer of 6 u64), see ptv_debug_counters()
+// Diagnostics (ptv_debug_stamps): when set, KMAX=8 launches use the STAMP instantiation,
+// which writes one record of kStampFields u64 per wave (s_memtime phase cycles + counts).
 unsigned long long *g_dbg = nullptr;
+long long g_dbg_cap = 0;  // records
 
 struct KnnKernelArgs {
     CellGrid cg;
@@ -136,6 +139,15 @@ __device__ __forceinline__ int wave_max_i(int v) {
     for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
     return v;
 }
+__device__ __forceinline__ int wave_incl_max_scan_i(int v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int t = __shfl_up(v, o, 64);
+        if (lane >= o) v = max(v, t);
+    }
+    return v;
+}
 __device__ __forceinline__ int wave_incl_scan_i(int v) {
     const int lane = threadIdx.x & 63;
 #pragma unroll
@@ -181,8 +193,21 @@ __device__ __forceinline__ void insert(double (&bd)[KMAX], int (&bp)[KMAX], doub
 // min(a, b) for non-NaN operands without fmin's canonicalising v_max
 __device__ __forceinline__ double dmin(double a, double b) { return a < b ? a : b; }
 
+// fp32 prefilter threshold: every candidate whose exact d2 is < thr has fp32 d2 <= this
+// (thr < 0: inactive lane, never; thr = inf: everything).
+__device__ __forceinline__ float f32_bound(double thr, double cpass) {
+    if (thr < 0.0) return -1.0f;
+    return (float)((thr * (1.0 + 9.5367431640625e-07) + cpass) * (1.0 + 2.384185791015625e-07));
+}
+
 __device__ __forceinline__ int clampi(double f, int n) {
     return f < 0.0 ? 0 : (f >= (double)(n - 1) ? n - 1 : (int)f);
+}
+
+// an upper bound on sqrt(x), x >= 0, from the fp32 square root (any over-estimate of a
+// gather half-width only adds cells; the same inputs always give the same bound)
+__device__ __forceinline__ double sqrt_up(double x) {
+    return (double)sqrtf((float)(x * (1.0 + 2.384185791015625e-07))) * (1.0 + 4.76837158203125e-07);
 }
 
 // distance between the extent [lo, hi] of a query box and cell c of an axis
@@ -192,7 +217,7 @@ __device__ __forceinline__ double axis_gap(int c, double o, double cs, double lo
     return fmax(fmax(c0 - hi, lo - c1), 0.0);
 }
 
-template <int KMAX>
+template <int KMAX, bool STAMP>
 __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const double4 *__restrict__ prec,
                                                     const double4 *__restrict__ pval,
                                                     const uint32_t *__restrict__ cstart,
@@ -201,13 +226,26 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
                                                     const double *__restrict__ qpy, const double *__restrict__ qpz,
                                                     const uint8_t *__restrict__ mask, double *__restrict__ U,
                                                     double *__restrict__ V, double *__restrict__ W,
-                                                    unsigned long long *__restrict__ dbg) {
+                                                    unsigned long long *__restrict__ dbg, long long dbg_cap) {
+    unsigned long long t_mark = 0, t_setup = 0, t_rows = 0, t_copy = 0, t_comp = 0, t_epi = 0;
+    auto stamp = [&](unsigned long long &acc) {
+        if constexpr (STAMP) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            acc += t - t_mark;
+            t_mark = t;
+        }
+    };
+    if constexpr (STAMP) t_mark = __builtin_amdgcn_s_memtime();
     __shared__ double4 lds_cand[4][kCap];
+    __shared__ float4 lds_candf[4][kCap];
     __shared__ uint2 lds_runs[4][kRunEntries];
+    __shared__ int lds_owner[4][kCap];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     double4 *buf = lds_cand[wid];
+    float4 *fbuf = lds_candf[wid];
     uint2 *runs = lds_runs[wid];
+    int *owner = lds_owner[wid];
     const int b = blockIdx.x;
     int ix, iy, iz;
     if (a.point_per_wave) {
@@ -247,6 +285,7 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
     // upper bound on this voxel's k-th distance from the coarse lattice (triangle inequality)
     double ub = INFINITY;
     if (a.cb.dk != nullptr && active) {
+        // |v - c| in fp32 from lattice-relative offsets, rounded up: any upper bound is valid
         const int st = a.cb.step;
         const int j0[3] = {cx / st, cy / st, (cz - a.z0) / st};
 #pragma unroll
@@ -254,11 +293,12 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
             const int jx = min(j0[0] + (c & 1), a.cb.n[0] - 1);
             const int jy = min(j0[1] + ((c >> 1) & 1), a.cb.n[1] - 1);
             const int jz = min(j0[2] + (c >> 2), a.cb.n[2] - 1);
-            const double ex = qx - a.cb.ax[jx], ey = qy - a.cb.ay[jy], ez = qz - a.cb.az[jz];
+            const float ex = (float)(qx - a.cb.ax[jx]), ey = (float)(qy - a.cb.ay[jy]), ez = (float)(qz - a.cb.az[jz]);
+            const float e2 = __fmaf_rn(ez, ez, __fmaf_rn(ey, ey, ex * ex));
             const double D = a.cb.dk[((size_t)jz * a.cb.n[1] + jy) * a.cb.n[0] + jx];
-            ub = fmin(ub, D + sqrt((ex * ex + ey * ey) + ez * ez));
+            ub = fmin(ub, D + (double)(sqrtf(e2) * 1.000002f));
         }
-        ub = ub * (1.0 + 1e-12) + a.cg.mg;
+        ub = ub * (1.0 + 1e-9) + a.cg.mg;
     }
     // candidates at or beyond the bound can never be among the k nearest
     const double ub2 = !active ? -1.0 : (ub < INFINITY ? ub * ub : INFINITY);
@@ -276,21 +316,38 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
     double thr = dmin(bd[KMAX - 1], ub2);
     uint32_t n_pass = 0, n_round = 0, n_rows = 0, n_cand = 0, n_acc = 0;
 
+    stamp(t_setup);
     if (__builtin_amdgcn_ballot_w64(active) != 0) {
         const double bx0 = uniform(wave_min(active ? qx : INFINITY)), bx1 = uniform(wave_max(active ? qx : -INFINITY));
         const double by0 = uniform(wave_min(active ? qy : INFINITY)), by1 = uniform(wave_max(active ? qy : -INFINITY));
         const double bz0 = uniform(wave_min(active ? qz : INFINITY)), bz1 = uniform(wave_max(active ? qz : -INFINITY));
         const CellGrid &g = a.cg;
+        // tile centre: candidates and voxels get fp32 coordinates relative to it
+        const double tcx = uniform(0.5 * (bx0 + bx1)), tcy = uniform(0.5 * (by0 + by1)), tcz = uniform(0.5 * (bz0 + bz1));
+        const float qfx = (float)(qx - tcx), qfy = (float)(qy - tcy), qfz = (float)(qz - tcz);
+        const double bhalf = 0.5 * sqrt(((bx1 - bx0) * (bx1 - bx0) + (by1 - by0) * (by1 - by0)) + (bz1 - bz0) * (bz1 - bz0));
+        double cpass = 0.0;
+        float thrf = 0.f;
         double Rp = -1.0;  // radius already gathered (none yet)
         // R_ub covers every lane's k-th neighbour: small (fluid) -> try r0 first and then
         // the exact max k-th distance; large (void) -> one pass at R_ub.
         const double R_ub = uniform(wave_max(active ? ub : -INFINITY));
         double R = a.r0;
-        if (R_ub < INFINITY) R = fmin(R_ub, a.r0);
+        // a tight lattice bound (fine level) is used directly in one pass; a loose one
+        // (coarse level) is preceded by a pass at the density radius r0.
+        if (R_ub < INFINITY) R = (R_ub <= 2.0 * a.r0) ? R_ub : a.r0;
         int py0 = 1, py1 = 0, pz0 = 1, pz1 = 0;  // row box of the previous pass (empty)
         while (true) {
             ++n_pass;
             const double Rg = R + g.mg, Rg2 = Rg * Rg;
+            {
+                // |fp32 - exact| distance error <= delta = M * 2^-21 for coordinates within M of the
+                // tile centre; (s + delta)^2 <= s^2 + 2 M delta + delta^2 bounds the test.
+                const double M = Rg + 2.0 * bhalf + 2.0 * fmax(g.cs[0], fmax(g.cs[1], g.cs[2]));
+                const double delta = M * 4.76837158203125e-07;
+                cpass = 2.0 * M * delta + delta * delta;
+                thrf = f32_bound(thr, cpass);
+            }
             const double Rpg2 = Rp < 0.0 ? -1.0 : (Rp + g.mg) * (Rp + g.mg);
             const int ry0 = clampi(floor((by0 - Rg - g.o[1]) * g.ic[1]), g.nc[1]);
             const int ry1 = clampi(floor((by1 + Rg - g.o[1]) * g.ic[1]), g.nc[1]);
@@ -298,6 +355,7 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
             const int rz1 = clampi(floor((bz1 + Rg - g.o[2]) * g.ic[2]), g.nc[2]);
             const int nyr = ry1 - ry0 + 1;
             const int nrows = nyr * (rz1 - rz0 + 1);
+            const float inv_nyr = 1.0f / (float)nyr;
             for (int rb = 0; rb < nrows; rb += 64 * kRowsPerLane) {
                 ++n_round;
                 // ---- lane = kRowsPerLane cell rows: x-runs of this shell -> particle ranges ----
@@ -309,18 +367,21 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
                     rs[2 * q] = rs[2 * q + 1] = 0;
                     rc[2 * q] = rc[2 * q + 1] = 0;
                     if (row < nrows) {
-                        const int ccy = ry0 + row % nyr, ccz = rz0 + row / nyr;
+                        int rq = (int)((float)row * inv_nyr);  // row / nyr without an integer divide
+                        rq -= (rq * nyr > row) ? 1 : 0;
+                        rq += ((rq + 1) * nyr <= row) ? 1 : 0;
+                        const int ccy = ry0 + (row - rq * nyr), ccz = rz0 + rq;
                         const double gy = axis_gap(ccy, g.o[1], g.cs[1], by0, by1);
                         const double gz = axis_gap(ccz, g.o[2], g.cs[2], bz0, bz1);
                         const double h2 = gy * gy + gz * gz;
                         if (h2 <= Rg2) {
-                            const double rx = sqrt(Rg2 - h2);
+                            const double rx = sqrt_up(Rg2 - h2);
                             const int a1 = clampi(floor((bx0 - rx - g.o[0]) * g.ic[0]), g.nc[0]);
                             const int b1 = clampi(floor((bx1 + rx - g.o[0]) * g.ic[0]), g.nc[0]);
                             int lo1 = a1, hi1 = b1, lo2 = 1, hi2 = 0;  // [lo, hi] inclusive runs
                             if (h2 <= Rpg2 && ccy >= py0 && ccy <= py1 && ccz >= pz0 && ccz <= pz1) {
                                 // row was gathered by the previous pass: only the x extensions are new
-                                const double rxo = sqrt(Rpg2 - h2);
+                                const double rxo = sqrt_up(Rpg2 - h2);
                                 const int a0 = clampi(floor((bx0 - rxo - g.o[0]) * g.ic[0]), g.nc[0]);
                                 const int b0 = clampi(floor((bx1 + rxo - g.o[0]) * g.ic[0]), g.nc[0]);
                                 hi1 = a0 - 1;
@@ -353,39 +414,66 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
                     pre += rc[r];
                 }
                 wave_lds_sync();
+                stamp(t_rows);
                 for (int cb = 0; cb < total; cb += kCap) {
-                    // ---- copy candidates [cb, cb + nc) into this wave's LDS buffer: lane i takes
-                    //      candidate cb + i + 64 t, finds its run by binary search in the run table
-                    //      (last entry with first index <= candidate), loads the record ----
+                    // ---- copy candidates [cb, cb + nc) into this wave's LDS buffer.  Each run marks
+                    //      its first chunk position with its id (ids grow with candidate order), a
+                    //      prefix max gives every position its run, lane i copies positions i, i+64 ----
                     const int nc = min(kCap, total - cb);
 #pragma unroll
-                    for (int t = 0; t < kCap / 64; ++t) {
-                        const int i = cb + t * 64 + lane;
-                        if (t * 64 < nc && i < cb + nc) {
-                            int e = 0;
+                    for (int t = 0; t < kCap / 64; ++t) owner[t * 64 + lane] = -1;
+                    wave_lds_sync();
 #pragma unroll
-                            for (int stp = kRunEntries / 2; stp > 0; stp >>= 1)
-                                if ((int)runs[e + stp].x <= i) e += stp;
-                            const uint2 rn = runs[e];
-                            const uint32_t slot = rn.y + (uint32_t)(i - (int)rn.x);
+                    for (int r = 0, pre = off; r < 2 * kRowsPerLane; ++r) {
+                        if (rc[r] > 0 && pre < cb + kCap && pre + rc[r] > cb)
+                            owner[max(pre, cb) - cb] = lane * 2 * kRowsPerLane + r;
+                        pre += rc[r];
+                    }
+                    wave_lds_sync();
+                    int carry = -1;
+#pragma unroll
+                    for (int t = 0; t < kCap / 64; ++t) {
+                        const int i = t * 64 + lane;
+                        const int o = max(wave_incl_max_scan_i(owner[i]), carry);
+                        carry = __builtin_amdgcn_readlane(o, 63);
+                        if (i < nc) {
+                            const uint2 rn = runs[o];
+                            const uint32_t slot = rn.y + (uint32_t)(i + cb - (int)rn.x);
                             const double4 p4 = prec[slot];
-                            buf[i - cb] = make_double4(p4.x, p4.y, p4.z, __longlong_as_double((long long)slot));
+                            buf[i] = make_double4(p4.x, p4.y, p4.z, __longlong_as_double((long long)slot));
+                            fbuf[i] = make_float4((float)(p4.x - tcx), (float)(p4.y - tcy), (float)(p4.z - tcz), 0.f);
                         }
                     }
                     wave_lds_sync();
-                    // ---- every candidate against all 64 voxels ----
-                    for (int i = 0; i < nc; ++i) {
-                        const double4 c = buf[i];
-                        const double dx = qx - c.x, dy = qy - c.y, dz = qz - c.z;
-                        const double d2 = (dx * dx + dy * dy) + dz * dz;
-                        if (__builtin_amdgcn_ballot_w64(d2 < thr) != 0) {  // wave-uniform
-                            ++n_acc;
-                            insert<KMAX>(bd, bp, d2, (int)__double_as_longlong(c.w));  // no-op where d2 >= thr
-                            thr = dmin(bd[KMAX - 1], ub2);
+                    stamp(t_copy);
+                    // ---- every candidate against all 64 voxels: fp32 prefilter on tile-relative
+                    //      coordinates, exact fp64 d2 + insertion only where some lane may improve ----
+                    for (int i0 = 0; i0 < nc; i0 += 4) {
+                        float d2f[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const float4 f = fbuf[min(i0 + u, nc - 1)];
+                            const float ex = qfx - f.x, ey = qfy - f.y, ez = qfz - f.z;
+                            d2f[u] = __fmaf_rn(ez, ez, __fmaf_rn(ey, ey, ex * ex));
+                        }
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            if (i0 + u < nc && __builtin_amdgcn_ballot_w64(d2f[u] <= thrf) != 0) {
+                                const double4 c = buf[i0 + u];
+                                const double dx = qx - c.x, dy = qy - c.y, dz = qz - c.z;
+                                const double d2 = (dx * dx + dy * dy) + dz * dz;
+                                if (__builtin_amdgcn_ballot_w64(d2 < thr) != 0) {  // wave-uniform
+                                    ++n_acc;
+                                    insert<KMAX>(bd, bp, d2, (int)__double_as_longlong(c.w));  // no-op where d2 >= thr
+                                    thr = dmin(bd[KMAX - 1], ub2);
+                                    thrf = f32_bound(thr, cpass);
+                                }
+                            }
                         }
                     }
                     n_cand += (uint32_t)nc;
                     wave_lds_sync();
+                    stamp(t_comp);
                 }
             }
             // ---- exactness: lanes with k-th distance <= R are final ----
@@ -413,14 +501,7 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
             R = fmin(R, a.rall);
         }
     }
-    if (dbg != nullptr && lane == 0) {
-        atomicAdd(dbg + 0, 1ull);
-        atomicAdd(dbg + 1, (unsigned long long)n_pass);
-        atomicAdd(dbg + 2, (unsigned long long)n_round);
-        atomicAdd(dbg + 3, (unsigned long long)n_cand);
-        atomicAdd(dbg + 4, (unsigned long long)n_acc);
-    }
-    if (dbg != nullptr) atomicAdd(dbg + 5, (unsigned long long)n_rows);
+    stamp(t_setup);  // exactness checks / radius updates count as setup
 
     if (!valid) return;
     const size_t vo = ((size_t)(iz - a.z0) * a.ny + iy) * a.nx + ix;
@@ -500,6 +581,21 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
     U[vo] = out[0];
     V[vo] = out[1];
     W[vo] = out[2];
+    if constexpr (STAMP) {
+        stamp(t_epi);
+        const long long gw = (long long)blockIdx.x * 4 + wid;
+        if (dbg != nullptr && gw < dbg_cap && (threadIdx.x & 63) == (int)__builtin_ffsll((long long)__builtin_amdgcn_ballot_w64(true)) - 1) {
+            unsigned long long *r = dbg + gw * kStampFields;
+            r[0] = t_setup;
+            r[1] = t_rows;
+            r[2] = t_copy;
+            r[3] = t_comp;
+            r[4] = t_epi;
+            r[5] = n_cand;
+            r[6] = n_acc;
+            r[7] = n_round + ((unsigned long long)n_pass << 32);
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -608,8 +704,15 @@ template <int KMAX>
 static void launch_t(dim3 grid, hipStream_t s, const KnnKernelArgs &ka, const Binned &b, const double *ax,
                      const double *ay, const double *az, const double *qx, const double *qy, const double *qz,
                      const uint8_t *mask, double *U, double *V, double *W) {
-    hipLaunchKernelGGL(k_knn_interp<KMAX>, grid, dim3(256), 0, s, ka, b.prec, b.pval, b.cstart, ax, ay, az, qx, qy,
-                       qz, mask, U, V, W, g_dbg);
+    if constexpr (KMAX == 8) {
+        if (g_dbg != nullptr && ka.mode == kModeInterp) {
+            hipLaunchKernelGGL((k_knn_interp<KMAX, true>), grid, dim3(256), 0, s, ka, b.prec, b.pval, b.cstart, ax, ay,
+                               az, qx, qy, qz, mask, U, V, W, g_dbg, g_dbg_cap);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((k_knn_interp<KMAX, false>), grid, dim3(256), 0, s, ka, b.prec, b.pval, b.cstart, ax, ay, az,
+                       qx, qy, qz, mask, U, V, W, (unsigned long long *)nullptr, 0LL);
 }
 
 int launch_knn(const KnnLaunch &a, const Binned &b, const double *ax, const double *ay, const double *az,

@@ -12,7 +12,7 @@ for f in sorted(glob.glob(f"{root}/**/*counter_collection.csv", recursive=True))
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
         key = "knn" if "knn_interp" in name else name[:40]
-        g = int(r["Grid_Size"])
+        g = int(r.get("Grid_Size", r.get("Grid_Size_X", 0)))
         if key == "knn":
             key = f"knn(grid={g})"
         agg[key][r["Counter_Name"]] += float(r["Counter_Value"])

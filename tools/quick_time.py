@@ -16,14 +16,15 @@ t = time.time(); P, Q = synth.sphere_pack(N, G); print("synth", round(time.time(
 ax = np.linspace(0, G - 1, G)
 ctx = _lib.Context.get(0)
 for it in range(3):
-    if "--counters" in sys.argv and it == 2:
-        ctx.debug_counters(1)
+    if "--stamps" in sys.argv and it == 2:
+        ctx.debug_stamps(1)
     t = time.time()
     U, V, W = ctx.interp_knn(P, Q, axes=(ax, ax, ax), k=k, cell_occupancy=occ)
     st = ctx.stats
     print(f"iter {it} G {G} N {N} k {k} occ {occ} wall {time.time()-t:.3f}s bin {st['ms_bin']:.2f} ms lat {st['ms_lattice']:.2f} ms knn {st['ms_knn']:.2f} ms "
           f"cells {st['cells']} r0 {st['r0']:.2f} Mvox/s(knn) {G**3/st['ms_knn']/1e3:.1f}", flush=True)
-if "--counters" in sys.argv:
-    c = ctx.debug_counters(2); ctx.debug_counters(0)
-    w = max(c["waves"], 1)
-    print("counters per wave:", {k2: round(v / w, 2) for k2, v in c.items()}, "waves", c["waves"])
+if "--stamps" in sys.argv:
+    c = ctx.debug_stamps(2); ctx.debug_stamps(0)
+    print("waves recorded", int(c["waves"]))
+    print("mean per wave:", {k2: round(v, 1) for k2, v in c["mean"].items()})
+    print("max  per wave:", {k2: round(v, 1) for k2, v in c["max"].items()})
