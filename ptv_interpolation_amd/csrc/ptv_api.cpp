@@ -65,6 +65,7 @@ struct ptv_ctx {
     DevBuf<double> bbox_part, bbox_out;
     DevBuf<unsigned long long> dbg;
     DevBuf<double> lat_axes[kMaxLattice], lat_dk[kMaxLattice];  // coarse-lattice bound levels
+    DevBuf<uint32_t> lat_slots[kMaxLattice];                     // their k-NN lists (seeds)
     double *h_bbox = nullptr;  // pinned, 6 doubles
     ptv_stats last{};
 };
@@ -153,6 +154,7 @@ int ptv_free(ptv_ctx *c) {
     c->dbg.release();
     for (auto &b : c->lat_axes) b.release();
     for (auto &b : c->lat_dk) b.release();
+    for (auto &b : c->lat_slots) b.release();
     if (c->h_bbox) hipHostFree(c->h_bbox);
     hipEventDestroy(c->ev_knn0);
     hipEventDestroy(c->ev_knn1);
@@ -168,7 +170,7 @@ int ptv_free(ptv_ctx *c) {
 
 namespace {
 
-constexpr double kDefaultOccupancy = 0.35;  // particles per binning cell
+constexpr double kDefaultOccupancy = 1.2;  // particles per binning cell
 constexpr double kDefaultR0Scale = 1.0;     // first gather radius / expected k-NN radius
 constexpr long long kMaxCells = 1LL << 28;
 constexpr int kLatticeStep = 4;                 // coarse lattice = every 4th grid point (+ last)
@@ -340,6 +342,7 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
     struct Lat {
         int n[3];
         double *ax, *ay, *az, *dk;
+        uint32_t *slots;  // NULL on the coarsest (count-bound) level
     };
     Lat lat[kMaxLattice];
     int nlat = 0;
@@ -357,6 +360,7 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
             L.ay = L.ax + L.n[0];
             L.az = L.ay + L.n[1];
             L.dk = c->lat_dk[nlat].p;
+            L.slots = nullptr;
             double *dst[3] = {L.ax, L.ay, L.az};
             for (int d = 0; d < 3; ++d) PTV_TRY(launch_subsample(src[d], n[d], kLatticeStep, dst[d], L.n[d], s));
             for (int d = 0; d < 3; ++d) {
@@ -391,7 +395,10 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
                                        lat[l].n[2], prm->k, kl.r0, lat[l].dk, s));
             continue;
         }
+        PTV_TRY(c->lat_slots[l].ensure((size_t)lat[l].n[0] * lat[l].n[1] * lat[l].n[2] * prm->k));
+        lat[l].slots = c->lat_slots[l].p;
         KnnLaunch ll = kl;
+        ll.kd_slots = lat[l].slots;
         ll.nx = lat[l].n[0];
         ll.ny = lat[l].n[1];
         ll.nz = lat[l].n[2];
@@ -403,6 +410,7 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
         ll.cb.ay = lat[l + 1].ay;
         ll.cb.az = lat[l + 1].az;
         ll.cb.dk = lat[l + 1].dk;
+        ll.cb.slots = lat[l + 1].slots;
         for (int d = 0; d < 3; ++d) ll.cb.n[d] = lat[l + 1].n[d];
         ll.cb.step = kLatticeStep;
         PTV_TRY(launch_knn(ll, b, lat[l].ax, lat[l].ay, lat[l].az, nullptr, nullptr, nullptr, nullptr, lat[l].dk,
@@ -413,6 +421,7 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
         kl.cb.ay = lat[0].ay;
         kl.cb.az = lat[0].az;
         kl.cb.dk = lat[0].dk;
+        kl.cb.slots = lat[0].slots;
         for (int d = 0; d < 3; ++d) kl.cb.n[d] = lat[0].n[d];
         kl.cb.step = kLatticeStep;
     }

@@ -27,6 +27,7 @@ size_t scan_partials_needed(size_t m);
 struct CoarseBound {
     const double *ax = nullptr, *ay = nullptr, *az = nullptr;  // lattice axes
     const double *dk = nullptr;                                // (n[2], n[1], n[0]) k-th distances
+    const uint32_t *slots = nullptr;  // (n[2], n[1], n[0], k) k-NN particle slots, or NULL (count bound)
     int n[3] = {0, 0, 0};
     int step = 4;
 };
@@ -47,6 +48,7 @@ struct KnnLaunch {
     int mode = kModeInterp;
     int point_per_wave = 0;  // 1: one grid point per wave (coarsest lattice)
     CoarseBound cb;
+    uint32_t *kd_slots = nullptr;  // kModeKDist: also write each point's k-NN slots here
 };
 
 // Upper bound on the k-th neighbour distance of every point of a separable grid by

@@ -43,13 +43,15 @@ namespace ptv {
 
 constexpr int kStampFields = 8;
 constexpr int kCap = 128;        // LDS candidate slots per wave (16 B fp32 + 32 B fp64 each)
-constexpr int kRowsPerLane = 2;  // cell rows examined per lane per gather round
+constexpr int kRowsPerLane = 1;  // cell rows examined per lane per gather round
 constexpr int kRunEntries = 64 * 2 * kRowsPerLane;  // x-runs per gather round (power of two)
 
 // Diagnostics (ptv_debug_stamps): when set, KMAX=8 launches use the STAMP instantiation,
 // which writes one record of kStampFields u64 per wave (s_memtime phase cycles + counts).
 unsigned long long *g_dbg = nullptr;
 long long g_dbg_cap = 0;  // records
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 struct KnnKernelArgs {
     CellGrid cg;
@@ -63,6 +65,7 @@ struct KnnKernelArgs {
     int mode;     // kModeInterp / kModeKDist
     int point_per_wave;
     CoarseBound cb;
+    uint32_t *kd_slots;  // kModeKDist: k-NN slots out (NULL = none)
 };
 
 // numpy pairwise sum of a[0..n) (n <= KMAX <= 128), from identity 0.0.
@@ -210,6 +213,13 @@ __device__ __forceinline__ double sqrt_up(double x) {
     return (double)sqrtf((float)(x * (1.0 + 2.384185791015625e-07))) * (1.0 + 4.76837158203125e-07);
 }
 
+// bijection of [0, nb): block b (dispatched to XCD b % 8) -> a contiguous range per XCD
+__device__ __forceinline__ int xcd_block(int b, int nb) {
+    const int q = nb >> 3, r = nb & 7;
+    const int x = b & 7, i = b >> 3;
+    return (x < r) ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
+}
+
 // distance between the extent [lo, hi] of a query box and cell c of an axis
 __device__ __forceinline__ double axis_gap(int c, double o, double cs, double lo, double hi) {
     const double c0 = o + (double)c * cs;
@@ -237,16 +247,19 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
     };
     if constexpr (STAMP) t_mark = __builtin_amdgcn_s_memtime();
     __shared__ double4 lds_cand[4][kCap];
-    __shared__ float4 lds_candf[4][kCap];
+    __shared__ __attribute__((aligned(16))) float lds_cfx[4][kCap], lds_cfy[4][kCap], lds_cfz[4][kCap];
     __shared__ uint2 lds_runs[4][kRunEntries];
     __shared__ int lds_owner[4][kCap];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     double4 *buf = lds_cand[wid];
-    float4 *fbuf = lds_candf[wid];
+    float *fbx = lds_cfx[wid], *fby = lds_cfy[wid], *fbz = lds_cfz[wid];
     uint2 *runs = lds_runs[wid];
     int *owner = lds_owner[wid];
-    const int b = blockIdx.x;
+    // XCD-aware block order: the dispatcher deals workgroups round-robin over the 8 XCDs,
+    // so give XCD x a contiguous range of tiles (neighbouring tiles share cell rows and
+    // particle records; each XCD has its own L2)
+    const int b = xcd_block(blockIdx.x, gridDim.x);
     int ix, iy, iz;
     if (a.point_per_wave) {
         // every lane of the wave takes the same grid point (coarsest lattice: a point-sized
@@ -301,7 +314,7 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
         ub = ub * (1.0 + 1e-9) + a.cg.mg;
     }
     // candidates at or beyond the bound can never be among the k nearest
-    const double ub2 = !active ? -1.0 : (ub < INFINITY ? ub * ub : INFINITY);
+    double ub2 = !active ? -1.0 : (ub < INFINITY ? ub * ub : INFINITY);
 
     // sorted list: KMAX-k front sentinels (-1) so bd[KMAX-1] is the k-th best.
     // Inactive lanes (padding / solid voxels) hold -1 everywhere: they never accept a
@@ -314,6 +327,7 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
         bp[j] = -1;
     }
     double thr = dmin(bd[KMAX - 1], ub2);
+
     uint32_t n_pass = 0, n_round = 0, n_rows = 0, n_cand = 0, n_acc = 0;
 
     stamp(t_setup);
@@ -325,7 +339,88 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
         // tile centre: candidates and voxels get fp32 coordinates relative to it
         const double tcx = uniform(0.5 * (bx0 + bx1)), tcy = uniform(0.5 * (by0 + by1)), tcz = uniform(0.5 * (bz0 + bz1));
         const float qfx = (float)(qx - tcx), qfy = (float)(qy - tcy), qfz = (float)(qz - tcz);
+        const f32x2 qf2x = {qfx, qfx}, qf2y = {qfy, qfy}, qf2z = {qfz, qfz};
         const double bhalf = 0.5 * sqrt(((bx1 - bx0) * (bx1 - bx0) + (by1 - by0) * (by1 - by0)) + (bz1 - bz0) * (bz1 - bz0));
+        bool seeded = false;
+        if constexpr (KMAX <= 8) {
+            if (a.cb.slots != nullptr && !a.point_per_wave) {
+                // ---- seeds: the k-NN lists of the tile's 8 coarse-lattice corners.  Every lane's
+                //      k-th smallest distance to their (deduplicated) union bounds its k-th
+                //      neighbour distance from above, usually to within a few ulps, so the gather
+                //      radius is tight and one pass is exact. ----
+                const int st = a.cb.step;
+                const int jx0 = __builtin_amdgcn_readfirstlane(cx / st);
+                const int jy0 = __builtin_amdgcn_readfirstlane(cy / st);
+                const int jz0 = __builtin_amdgcn_readfirstlane((cz - a.z0) / st);
+                const int cc = lane >> 3, j = lane & 7;
+                const int jx = min(jx0 + (cc & 1), a.cb.n[0] - 1);
+                const int jy = min(jy0 + ((cc >> 1) & 1), a.cb.n[1] - 1);
+                const int jz = min(jz0 + (cc >> 2), a.cb.n[2] - 1);
+                uint32_t sl = 0xffffffffu;
+                if (j < a.k) sl = a.cb.slots[(((size_t)jz * a.cb.n[1] + jy) * a.cb.n[0] + jx) * a.k + j];
+                // bitonic sort of the 64 slots across the wave, then keep first occurrences
+#pragma unroll
+                for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+                    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                        const uint32_t o = (uint32_t)__shfl_xor((int)sl, stride, 64);
+                        const bool keep_min = ((lane & stride) == 0) == ((lane & size) == 0);
+                        sl = keep_min ? min(sl, o) : max(sl, o);
+                    }
+                }
+                const uint32_t prv = (uint32_t)__shfl_up((int)sl, 1, 64);
+                const bool uniq = sl != 0xffffffffu && (lane == 0 || sl != prv);
+                const unsigned long long um = __builtin_amdgcn_ballot_w64(uniq);
+                const int nu = __builtin_popcountll(um);
+                const int pos = __builtin_amdgcn_mbcnt_hi((unsigned)(um >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)um, 0u));
+                double pm = 0.0;
+                if (uniq) {
+                    const double4 p4 = prec[sl];
+                    const double ex = p4.x - tcx, ey = p4.y - tcy, ez = p4.z - tcz;
+                    fbx[pos] = (float)ex;
+                    fby[pos] = (float)ey;
+                    fbz[pos] = (float)ez;
+                    pm = fabs(ex) + fabs(ey) + fabs(ez);  // >= the Euclidean distance to the centre
+                }
+                // seed-voxel distances are <= Ms; fp32 distance error <= Ms * 2^-21 (as cpass below)
+                const double Ms = uniform(wave_max(pm)) + bhalf;
+                wave_lds_sync();
+                float sd[KMAX];
+#pragma unroll
+                for (int q = 0; q < KMAX; ++q) sd[q] = INFINITY;
+                for (int i = 0; i < nu; i += 2) {
+                    const float2 X = *reinterpret_cast<const float2 *>(fbx + i);
+                    const float2 Y = *reinterpret_cast<const float2 *>(fby + i);
+                    const float2 Z = *reinterpret_cast<const float2 *>(fbz + i);
+                    const f32x2 ex = qf2x - f32x2{X.x, X.y}, ey = qf2y - f32x2{Y.x, Y.y}, ez = qf2z - f32x2{Z.x, Z.y};
+                    f32x2 s2 = ex * ex;
+                    s2 = __builtin_elementwise_fma(ey, ey, s2);
+                    s2 = __builtin_elementwise_fma(ez, ez, s2);
+                    const float xs[2] = {s2.x, i + 1 < nu ? s2.y : INFINITY};
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+                        for (int q = KMAX - 1; q > 0; --q) sd[q] = __builtin_amdgcn_fmed3f(sd[q - 1], sd[q], xs[u]);
+                        sd[0] = fminf(sd[0], xs[u]);
+                    }
+                }
+                float kth = sd[0];
+#pragma unroll
+                for (int q = 1; q < KMAX; ++q)
+                    if (q == a.k - 1) kth = sd[q];
+                if (active && kth < INFINITY) {
+                    const double dl = Ms * 4.76837158203125e-07;
+                    const double st2 = ((double)kth * (1.0 + 9.5367431640625e-07) + (2.0 * Ms * dl + dl * dl)) * (1.0 + 1e-12);
+                    if (st2 < ub2) {
+                        ub2 = st2;
+                        ub = sqrt(st2) * (1.0 + 1e-12);
+                    }
+                }
+                seeded = true;
+                thr = dmin(bd[KMAX - 1], ub2);
+                wave_lds_sync();  // the gather reuses the candidate buffers
+            }
+        }
         double cpass = 0.0;
         float thrf = 0.f;
         double Rp = -1.0;  // radius already gathered (none yet)
@@ -335,7 +430,7 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
         double R = a.r0;
         // a tight lattice bound (fine level) is used directly in one pass; a loose one
         // (coarse level) is preceded by a pass at the density radius r0.
-        if (R_ub < INFINITY) R = (R_ub <= 2.0 * a.r0) ? R_ub : a.r0;
+        if (R_ub < INFINITY) R = (seeded || R_ub <= 2.0 * a.r0) ? R_ub : a.r0;
         int py0 = 1, py1 = 0, pz0 = 1, pz1 = 0;  // row box of the previous pass (empty)
         while (true) {
             ++n_pass;
@@ -353,8 +448,13 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
             const int ry1 = clampi(floor((by1 + Rg - g.o[1]) * g.ic[1]), g.nc[1]);
             const int rz0 = clampi(floor((bz0 - Rg - g.o[2]) * g.ic[2]), g.nc[2]);
             const int rz1 = clampi(floor((bz1 + Rg - g.o[2]) * g.ic[2]), g.nc[2]);
-            const int nyr = ry1 - ry0 + 1;
-            const int nrows = nyr * (rz1 - rz0 + 1);
+            // rows are visited centre-out (zigzag in y within zigzag in z around the tile's
+            // cell) so that near candidates come first and the k-th distances tighten early
+            const int cyc = clampi(floor((tcy - g.o[1]) * g.ic[1]), g.nc[1]);
+            const int czc = clampi(floor((tcz - g.o[2]) * g.ic[2]), g.nc[2]);
+            const int hy = max(cyc - ry0, ry1 - cyc), hz = max(czc - rz0, rz1 - czc);
+            const int nyr = 2 * hy + 1;
+            const int nrows = nyr * (2 * hz + 1);
             const float inv_nyr = 1.0f / (float)nyr;
             for (int rb = 0; rb < nrows; rb += 64 * kRowsPerLane) {
                 ++n_round;
@@ -370,11 +470,13 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
                         int rq = (int)((float)row * inv_nyr);  // row / nyr without an integer divide
                         rq -= (rq * nyr > row) ? 1 : 0;
                         rq += ((rq + 1) * nyr <= row) ? 1 : 0;
-                        const int ccy = ry0 + (row - rq * nyr), ccz = rz0 + rq;
+                        const int ty = row - rq * nyr;
+                        const int ccy = cyc + ((ty & 1) ? ((ty + 1) >> 1) : -(ty >> 1));
+                        const int ccz = czc + ((rq & 1) ? ((rq + 1) >> 1) : -(rq >> 1));
                         const double gy = axis_gap(ccy, g.o[1], g.cs[1], by0, by1);
                         const double gz = axis_gap(ccz, g.o[2], g.cs[2], bz0, bz1);
                         const double h2 = gy * gy + gz * gz;
-                        if (h2 <= Rg2) {
+                        if (h2 <= Rg2 && ccy >= ry0 && ccy <= ry1 && ccz >= rz0 && ccz <= rz1) {
                             const double rx = sqrt_up(Rg2 - h2);
                             const int a1 = clampi(floor((bx0 - rx - g.o[0]) * g.ic[0]), g.nc[0]);
                             const int b1 = clampi(floor((bx1 + rx - g.o[0]) * g.ic[0]), g.nc[0]);
@@ -441,7 +543,9 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
                             const uint32_t slot = rn.y + (uint32_t)(i + cb - (int)rn.x);
                             const double4 p4 = prec[slot];
                             buf[i] = make_double4(p4.x, p4.y, p4.z, __longlong_as_double((long long)slot));
-                            fbuf[i] = make_float4((float)(p4.x - tcx), (float)(p4.y - tcy), (float)(p4.z - tcz), 0.f);
+                            fbx[i] = (float)(p4.x - tcx);
+                            fby[i] = (float)(p4.y - tcy);
+                            fbz[i] = (float)(p4.z - tcz);
                         }
                     }
                     wave_lds_sync();
@@ -449,13 +553,20 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
                     // ---- every candidate against all 64 voxels: fp32 prefilter on tile-relative
                     //      coordinates, exact fp64 d2 + insertion only where some lane may improve ----
                     for (int i0 = 0; i0 < nc; i0 += 4) {
-                        float d2f[4];
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            const float4 f = fbuf[min(i0 + u, nc - 1)];
-                            const float ex = qfx - f.x, ey = qfy - f.y, ez = qfz - f.z;
-                            d2f[u] = __fmaf_rn(ez, ez, __fmaf_rn(ey, ey, ex * ex));
-                        }
+                        // 4 candidates as two packed-fp32 pairs (v_pk_add / v_pk_mul / v_pk_fma);
+                        // slots past nc hold stale values and are never tested
+                        const float4 X = *reinterpret_cast<const float4 *>(fbx + i0);
+                        const float4 Y = *reinterpret_cast<const float4 *>(fby + i0);
+                        const float4 Z = *reinterpret_cast<const float4 *>(fbz + i0);
+                        const f32x2 e0x = qf2x - f32x2{X.x, X.y}, e1x = qf2x - f32x2{X.z, X.w};
+                        const f32x2 e0y = qf2y - f32x2{Y.x, Y.y}, e1y = qf2y - f32x2{Y.z, Y.w};
+                        const f32x2 e0z = qf2z - f32x2{Z.x, Z.y}, e1z = qf2z - f32x2{Z.z, Z.w};
+                        f32x2 s0 = e0x * e0x, s1 = e1x * e1x;
+                        s0 = __builtin_elementwise_fma(e0y, e0y, s0);
+                        s1 = __builtin_elementwise_fma(e1y, e1y, s1);
+                        s0 = __builtin_elementwise_fma(e0z, e0z, s0);
+                        s1 = __builtin_elementwise_fma(e1z, e1z, s1);
+                        const float d2f[4] = {s0.x, s0.y, s1.x, s1.y};
 #pragma unroll
                         for (int u = 0; u < 4; ++u) {
                             if (i0 + u < nc && __builtin_amdgcn_ballot_w64(d2f[u] <= thrf) != 0) {
@@ -494,7 +605,7 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
                 // shell does not overshoot the lens of particles the voxels actually need.
                 bool seen = false;
 #pragma unroll
-                for (int j = 0; j < KMAX; ++j) seen = seen || (bd[j] >= 0.0 && bd[j] < INFINITY);
+                for (int j = 0; j < KMAX; ++j) seen = seen || bp[j] >= 0;
                 const bool any_seen = __builtin_amdgcn_ballot_w64(seen) != 0;
                 R = any_seen ? R + fmax(a.r0, 0.125 * R) : 1.5 * R;
             }
@@ -507,6 +618,13 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
     const size_t vo = ((size_t)(iz - a.z0) * a.ny + iy) * a.nx + ix;
     if (a.mode == kModeKDist) {
         U[vo] = sqrt(bd[KMAX - 1]);
+        if (a.kd_slots != nullptr) {
+            // the k-NN slots (list order) seed the next finer level's tiles
+            uint32_t *o = a.kd_slots + vo * (size_t)a.k;
+#pragma unroll
+            for (int j = 0; j < KMAX; ++j)
+                if (j >= a.kpad) o[j - a.kpad] = (uint32_t)bp[j];
+        }
         return;
     }
     if (!active) {
@@ -746,6 +864,7 @@ int launch_knn(const KnnLaunch &a, const Binned &b, const double *ax, const doub
     ka.mode = a.mode;
     ka.point_per_wave = a.point_per_wave;
     ka.cb = a.cb;
+    ka.kd_slots = a.kd_slots;
     double diag2 = 0.0;
     for (int d = 0; d < 3; ++d) {
         const double e = a.cg.cs[d] * a.cg.nc[d];
