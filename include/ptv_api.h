@@ -139,11 +139,12 @@ int ptv_last_stats(ptv_ctx *ctx, ptv_stats *st);
 /*
  * Diagnostics: mode 1 = enable + zero per-wave phase stamps of the k-NN kernel (k <= 8
  * launches switch to an s_memtime-stamped build), 0 = disable, other = leave.  If out
- * != NULL (19 doubles) it receives {waves recorded, mean[9], max[9]} over the fields
- * {setup, rows, copy, compute, epilogue cycles, candidates, accepted, rounds, passes}.
+ * != NULL (23 doubles) it receives {waves recorded, mean[11], max[11]} over the fields
+ * {setup, seeds, rows, copy, compute, epilogue cycles, gathered candidates, merge
+ * iterations, rounds, passes, candidates kept by the sub-ball filter}.
  * Profiling only: stamps perturb the schedule; never time a stamped run.
  */
-int ptv_debug_stamps(ptv_ctx *ctx, int mode, double *out19);
+int ptv_debug_stamps(ptv_ctx *ctx, int mode, double *out23);
 
 #ifdef __cplusplus
 }

@@ -176,11 +176,12 @@ class Context:
 
     def debug_stamps(self, mode=2):
         """mode 1: enable+zero, 0: disable, 2: read.  Per-wave phase cycles (mean / max)."""
-        out = (C.c_double * 19)()
+        out = (C.c_double * 23)()
         check(lib().ptv_debug_stamps(self.h, int(mode), out))
-        keys = ("setup", "rows", "copy", "compute", "epilogue", "candidates", "accepted", "rounds", "passes")
+        keys = ("setup", "seeds", "rows", "copy", "compute", "epilogue", "candidates", "merges", "rounds",
+                "passes", "kept")
         v = list(out)
-        return {"waves": v[0], "mean": dict(zip(keys, v[1:10])), "max": dict(zip(keys, v[10:19]))}
+        return {"waves": v[0], "mean": dict(zip(keys, v[1:12])), "max": dict(zip(keys, v[12:23]))}
 
     # -- host buffers ------------------------------------------------------
     def interp_knn(self, points, values, axes=None, grid_points=None, shape=None, method=METHOD_IDW, k=8,

@@ -588,26 +588,32 @@ int ptv_debug_stamps(ptv_ctx *c, int mode, double *out) {
         PTV_HIP(hipDeviceSynchronize());
         std::vector<unsigned long long> h((size_t)cap * nf);
         PTV_HIP(hipMemcpy(h.data(), c->dbg.p, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-        // out: [records, mean of 9 fields, max of 9 fields] (field 7 split into rounds, passes)
-        double sum[9] = {0}, mx[9] = {0};
+        // out: [records, mean of 11 fields, max of 11 fields]: 6 phase cycle counts, then
+        // gathered candidates, merge iterations, rounds, passes, candidates kept by the
+        // sub-ball filter (packed two or three to a u64 in fields 6 and 7)
+        constexpr int nv = 11;
+        double sum[nv] = {0}, mx[nv] = {0};
         long long nrec = 0;
         for (long long w = 0; w < cap; ++w) {
             const unsigned long long *r = &h[(size_t)w * nf];
-            if (r[0] == 0 && r[1] == 0 && r[4] == 0) continue;
+            if (r[0] == 0 && r[2] == 0 && r[5] == 0) continue;
             ++nrec;
-            double v[9];
-            for (int f = 0; f < 7; ++f) v[f] = (double)r[f];
-            v[7] = (double)(r[7] & 0xffffffffULL);
-            v[8] = (double)(r[7] >> 32);
-            for (int f = 0; f < 9; ++f) {
+            double v[nv];
+            for (int f = 0; f < 6; ++f) v[f] = (double)r[f];
+            v[6] = (double)(r[6] & 0xffffffffULL);
+            v[7] = (double)(r[6] >> 32);
+            v[8] = (double)(r[7] & 0xffffULL);
+            v[9] = (double)((r[7] >> 16) & 0xffffULL);
+            v[10] = (double)(r[7] >> 32);
+            for (int f = 0; f < nv; ++f) {
                 sum[f] += v[f];
                 mx[f] = std::max(mx[f], v[f]);
             }
         }
         out[0] = (double)nrec;
-        for (int f = 0; f < 9; ++f) {
+        for (int f = 0; f < nv; ++f) {
             out[1 + f] = nrec ? sum[f] / (double)nrec : 0.0;
-            out[10 + f] = mx[f];
+            out[1 + nv + f] = mx[f];
         }
     }
     return PTV_OK;

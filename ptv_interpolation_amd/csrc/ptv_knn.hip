@@ -228,7 +228,7 @@ __device__ __forceinline__ double axis_gap(int c, double o, double cs, double lo
 }
 
 template <int KMAX, bool STAMP>
-__global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const double4 *__restrict__ prec,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ? 4 : 1))) void k_knn_interp(KnnKernelArgs a, const double4 *__restrict__ prec,
                                                     const double4 *__restrict__ pval,
                                                     const uint32_t *__restrict__ cstart,
                                                     const double *__restrict__ ax, const double *__restrict__ ay,
@@ -237,7 +237,7 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
                                                     const uint8_t *__restrict__ mask, double *__restrict__ U,
                                                     double *__restrict__ V, double *__restrict__ W,
                                                     unsigned long long *__restrict__ dbg, long long dbg_cap) {
-    unsigned long long t_mark = 0, t_setup = 0, t_rows = 0, t_copy = 0, t_comp = 0, t_epi = 0;
+    unsigned long long t_mark = 0, t_setup = 0, t_seed = 0, t_rows = 0, t_copy = 0, t_comp = 0, t_epi = 0;
     auto stamp = [&](unsigned long long &acc) {
         if constexpr (STAMP) {
             const unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -249,7 +249,7 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
     __shared__ double4 lds_cand[4][kCap];
     __shared__ __attribute__((aligned(16))) float lds_cfx[4][kCap], lds_cfy[4][kCap], lds_cfz[4][kCap];
     __shared__ uint2 lds_runs[4][kRunEntries];
-    __shared__ int lds_owner[4][kCap];
+    __shared__ int lds_owner[4][64];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     double4 *buf = lds_cand[wid];
@@ -328,7 +328,7 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
     }
     double thr = dmin(bd[KMAX - 1], ub2);
 
-    uint32_t n_pass = 0, n_round = 0, n_rows = 0, n_cand = 0, n_acc = 0;
+    uint32_t n_pass = 0, n_round = 0, n_rows = 0, n_cand = 0, n_acc = 0, n_surv = 0;
 
     stamp(t_setup);
     if (__builtin_amdgcn_ballot_w64(active) != 0) {
@@ -419,6 +419,7 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
                 seeded = true;
                 thr = dmin(bd[KMAX - 1], ub2);
                 wave_lds_sync();  // the gather reuses the candidate buffers
+                stamp(t_seed);
             }
         }
         double cpass = 0.0;
@@ -431,6 +432,111 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
         // a tight lattice bound (fine level) is used directly in one pass; a loose one
         // (coarse level) is preceded by a pass at the density radius r0.
         if (R_ub < INFINITY) R = (seeded || R_ub <= 2.0 * a.r0) ? R_ub : a.r0;
+        // ---- sub-balls: the tile's 8 sub-boxes of 2x2x2 voxels (lanes differing in bits 0, 2, 4),
+        //      each with centre c_s and radius max_v sqrt(thr_v) + |v - c_s|: a candidate outside
+        //      every sub-ball can never enter any list (thresholds only shrink), so the copy drops it.
+        //      fp32 on tile-relative coordinates, inflated for round-off (any over-estimate is safe).
+        float sbx[2], sby[2], sbz[2], sbr2[8];  // sub-box s spans x-half s&1, y-half s>>1&1, z-half s>>2
+        double Mpass = 0.0;  // bound on |coordinate - tile centre| of this pass's candidates
+        auto subballs = [&]() {
+            float rv = thr < 0.0 ? -1.0f : sqrtf((float)(thr * (1.0 + 2.384185791015625e-07))) * 1.0000005f;
+            // extent of this lane's x-half (lanes agreeing in bit 1), y-half (bit 3), z-half (bit 5)
+            float mnx = qfx, mxx = qfx, mny = qfy, mxy = qfy, mnz = qfz, mxz = qfz;
+#pragma unroll
+            for (int o = 1; o <= 32; o <<= 1) {
+                if (o != 2) {
+                    mnx = fminf(mnx, __shfl_xor(mnx, o, 64));
+                    mxx = fmaxf(mxx, __shfl_xor(mxx, o, 64));
+                }
+                if (o != 8) {
+                    mny = fminf(mny, __shfl_xor(mny, o, 64));
+                    mxy = fmaxf(mxy, __shfl_xor(mxy, o, 64));
+                }
+                if (o != 32) {
+                    mnz = fminf(mnz, __shfl_xor(mnz, o, 64));
+                    mxz = fmaxf(mxz, __shfl_xor(mxz, o, 64));
+                }
+                if (o == 1 || o == 4 || o == 16) rv = fmaxf(rv, __shfl_xor(rv, o, 64));
+            }
+            const float ux = mxx - mnx, uy = mxy - mny, uz = mxz - mnz;
+            const float hd = 0.5f * sqrtf(__fmaf_rn(uz, uz, __fmaf_rn(uy, uy, ux * ux))) * 1.00001f;
+            const float Rs = (rv + hd) * 1.00001f + (float)(Mpass * 1e-6);
+            const float R2s = rv < 0.0f ? -1.0f : Rs * Rs;
+            const float cxs = 0.5f * (mnx + mxx), cys = 0.5f * (mny + mxy), czs = 0.5f * (mnz + mxz);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                sbx[h] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cxs), h << 1));
+                sby[h] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cys), h << 3));
+                sbz[h] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(czs), h << 5));
+            }
+#pragma unroll
+            for (int sb = 0; sb < 8; ++sb) {
+                const int L = ((sb & 1) << 1) | ((sb & 2) << 2) | ((sb & 4) << 3);
+                sbr2[sb] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(R2s), L));
+            }
+        };
+        int nbuf = 0;  // compacted candidates waiting in this wave's LDS buffer (uniform)
+        // ---- every buffered candidate against all 64 voxels, in groups of 32 candidates:
+        //      (1) a branch-free fp32 stream on tile-relative coordinates leaves each lane a bit
+        //          mask of the candidates that may beat its threshold;
+        //      (2) each lane then walks its own bits in candidate order: exact fp64 d2 and the
+        //          insertion network.  The wave runs (2) max-over-lanes-popcount times instead of
+        //          once per candidate any lane accepts. ----
+        auto flush = [&]() {
+            if (nbuf == 0) return;
+            wave_lds_sync();
+            for (int g0 = 0; g0 < nbuf; g0 += 32) {
+                const int ng = min(32, nbuf - g0);
+                // candidate g0 + j ends at bit nb - 1 - j (shift-in order keeps the loop rolled)
+                uint32_t m = 0u;
+                const int nb = (ng + 3) & ~3;
+#pragma unroll 1
+                for (int i0 = 0; i0 < ng; i0 += 4) {
+                    // 4 candidates as two packed-fp32 pairs (v_pk_add / v_pk_mul / v_pk_fma);
+                    // slots past nbuf hold stale values, their bits are cleared below
+                    const float4 X = *reinterpret_cast<const float4 *>(fbx + g0 + i0);
+                    const float4 Y = *reinterpret_cast<const float4 *>(fby + g0 + i0);
+                    const float4 Z = *reinterpret_cast<const float4 *>(fbz + g0 + i0);
+                    const f32x2 e0x = qf2x - f32x2{X.x, X.y}, e1x = qf2x - f32x2{X.z, X.w};
+                    const f32x2 e0y = qf2y - f32x2{Y.x, Y.y}, e1y = qf2y - f32x2{Y.z, Y.w};
+                    const f32x2 e0z = qf2z - f32x2{Z.x, Z.y}, e1z = qf2z - f32x2{Z.z, Z.w};
+                    f32x2 s0 = e0x * e0x, s1 = e1x * e1x;
+                    s0 = __builtin_elementwise_fma(e0y, e0y, s0);
+                    s1 = __builtin_elementwise_fma(e1y, e1y, s1);
+                    s0 = __builtin_elementwise_fma(e0z, e0z, s0);
+                    s1 = __builtin_elementwise_fma(e1z, e1z, s1);
+                    const uint32_t b4 = ((s0.x <= thrf) ? 8u : 0u) | ((s0.y <= thrf) ? 4u : 0u) |
+                                        ((s1.x <= thrf) ? 2u : 0u) | ((s1.y <= thrf) ? 1u : 0u);
+                    m = (m << 4) | b4;
+                }
+                m &= ~((1u << (nb - ng)) - 1u);  // stale slots past nbuf
+                const double4 *gbuf = buf + g0 + nb - 32;  // bit position p <-> gbuf[31 - p]
+                while (__builtin_amdgcn_ballot_w64(m != 0u) != 0) {
+                    ++n_acc;
+                    double d2 = INFINITY;
+                    int slot = -1;
+                    if (m != 0u) {
+                        const int lz = __builtin_clz(m);
+                        m ^= 0x80000000u >> lz;
+                        const double4 c = gbuf[lz];
+                        const double dx = qx - c.x, dy = qy - c.y, dz = qz - c.z;
+                        const double e2 = (dx * dx + dy * dy) + dz * dz;
+                        if (e2 < thr) {
+                            d2 = e2;
+                            slot = (int)__double_as_longlong(c.w);
+                        }
+                    }
+                    insert<KMAX>(bd, bp, d2, slot);  // no-op where d2 = inf
+                    thr = dmin(bd[KMAX - 1], ub2);
+                }
+                thrf = f32_bound(thr, cpass);
+            }
+            n_surv += (uint32_t)nbuf;
+            nbuf = 0;
+            wave_lds_sync();  // the buffer is refilled next
+            subballs();
+            stamp(t_comp);
+        };
         int py0 = 1, py1 = 0, pz0 = 1, pz1 = 0;  // row box of the previous pass (empty)
         while (true) {
             ++n_pass;
@@ -442,6 +548,8 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
                 const double delta = M * 4.76837158203125e-07;
                 cpass = 2.0 * M * delta + delta * delta;
                 thrf = f32_bound(thr, cpass);
+                Mpass = M;
+                subballs();
             }
             const double Rpg2 = Rp < 0.0 ? -1.0 : (Rp + g.mg) * (Rp + g.mg);
             const int ry0 = clampi(floor((by0 - Rg - g.o[1]) * g.ic[1]), g.nc[1]);
@@ -517,76 +625,61 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
                 }
                 wave_lds_sync();
                 stamp(t_rows);
-                for (int cb = 0; cb < total; cb += kCap) {
-                    // ---- copy candidates [cb, cb + nc) into this wave's LDS buffer.  Each run marks
-                    //      its first chunk position with its id (ids grow with candidate order), a
-                    //      prefix max gives every position its run, lane i copies positions i, i+64 ----
-                    const int nc = min(kCap, total - cb);
-#pragma unroll
-                    for (int t = 0; t < kCap / 64; ++t) owner[t * 64 + lane] = -1;
+                for (int src = 0; src < total; src += 64) {
+                    // ---- copy window [src, src + 64) of this round's candidates.  Each run marks its
+                    //      first window position with its id (ids grow with candidate order), a prefix
+                    //      max gives every lane its run; lane i loads candidate src + i and keeps it
+                    //      only if it lies in some sub-ball (compacted into the LDS buffer) ----
+                    owner[lane] = -1;
                     wave_lds_sync();
 #pragma unroll
                     for (int r = 0, pre = off; r < 2 * kRowsPerLane; ++r) {
-                        if (rc[r] > 0 && pre < cb + kCap && pre + rc[r] > cb)
-                            owner[max(pre, cb) - cb] = lane * 2 * kRowsPerLane + r;
+                        if (rc[r] > 0 && pre < src + 64 && pre + rc[r] > src)
+                            owner[max(pre, src) - src] = lane * 2 * kRowsPerLane + r;
                         pre += rc[r];
                     }
                     wave_lds_sync();
-                    int carry = -1;
+                    const int o = wave_incl_max_scan_i(owner[lane]);
+                    const int i = src + lane;
+                    bool keep = false;
+                    double4 p4 = make_double4(0.0, 0.0, 0.0, 0.0);
+                    uint32_t slot = 0;
+                    float ex = 0.f, ey = 0.f, ez = 0.f;
+                    if (i < total) {
+                        const uint2 rn = runs[o];
+                        slot = rn.y + (uint32_t)(i - (int)rn.x);
+                        p4 = prec[slot];
+                        ex = (float)(p4.x - tcx);
+                        ey = (float)(p4.y - tcy);
+                        ez = (float)(p4.z - tcz);
+                        float qx2[2], qy2[2], qz2[2];
 #pragma unroll
-                    for (int t = 0; t < kCap / 64; ++t) {
-                        const int i = t * 64 + lane;
-                        const int o = max(wave_incl_max_scan_i(owner[i]), carry);
-                        carry = __builtin_amdgcn_readlane(o, 63);
-                        if (i < nc) {
-                            const uint2 rn = runs[o];
-                            const uint32_t slot = rn.y + (uint32_t)(i + cb - (int)rn.x);
-                            const double4 p4 = prec[slot];
-                            buf[i] = make_double4(p4.x, p4.y, p4.z, __longlong_as_double((long long)slot));
-                            fbx[i] = (float)(p4.x - tcx);
-                            fby[i] = (float)(p4.y - tcy);
-                            fbz[i] = (float)(p4.z - tcz);
+                        for (int h = 0; h < 2; ++h) {
+                            const float dx = ex - sbx[h], dy = ey - sby[h], dz = ez - sbz[h];
+                            qx2[h] = dx * dx;
+                            qy2[h] = dy * dy;
+                            qz2[h] = dz * dz;
                         }
+#pragma unroll
+                        for (int sb = 0; sb < 8; ++sb)
+                            keep = keep || (qx2[sb & 1] + qy2[(sb >> 1) & 1]) + qz2[sb >> 2] <= sbr2[sb];
                     }
-                    wave_lds_sync();
+                    const unsigned long long km = __builtin_amdgcn_ballot_w64(keep);
+                    if (keep) {
+                        const int pos = nbuf + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(km >> 32),
+                                                                              __builtin_amdgcn_mbcnt_lo((unsigned)km, 0u));
+                        buf[pos] = make_double4(p4.x, p4.y, p4.z, __longlong_as_double((long long)slot));
+                        fbx[pos] = ex;
+                        fby[pos] = ey;
+                        fbz[pos] = ez;
+                    }
+                    nbuf += __builtin_popcountll(km);
+                    n_cand += (uint32_t)min(64, total - src);
                     stamp(t_copy);
-                    // ---- every candidate against all 64 voxels: fp32 prefilter on tile-relative
-                    //      coordinates, exact fp64 d2 + insertion only where some lane may improve ----
-                    for (int i0 = 0; i0 < nc; i0 += 4) {
-                        // 4 candidates as two packed-fp32 pairs (v_pk_add / v_pk_mul / v_pk_fma);
-                        // slots past nc hold stale values and are never tested
-                        const float4 X = *reinterpret_cast<const float4 *>(fbx + i0);
-                        const float4 Y = *reinterpret_cast<const float4 *>(fby + i0);
-                        const float4 Z = *reinterpret_cast<const float4 *>(fbz + i0);
-                        const f32x2 e0x = qf2x - f32x2{X.x, X.y}, e1x = qf2x - f32x2{X.z, X.w};
-                        const f32x2 e0y = qf2y - f32x2{Y.x, Y.y}, e1y = qf2y - f32x2{Y.z, Y.w};
-                        const f32x2 e0z = qf2z - f32x2{Z.x, Z.y}, e1z = qf2z - f32x2{Z.z, Z.w};
-                        f32x2 s0 = e0x * e0x, s1 = e1x * e1x;
-                        s0 = __builtin_elementwise_fma(e0y, e0y, s0);
-                        s1 = __builtin_elementwise_fma(e1y, e1y, s1);
-                        s0 = __builtin_elementwise_fma(e0z, e0z, s0);
-                        s1 = __builtin_elementwise_fma(e1z, e1z, s1);
-                        const float d2f[4] = {s0.x, s0.y, s1.x, s1.y};
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            if (i0 + u < nc && __builtin_amdgcn_ballot_w64(d2f[u] <= thrf) != 0) {
-                                const double4 c = buf[i0 + u];
-                                const double dx = qx - c.x, dy = qy - c.y, dz = qz - c.z;
-                                const double d2 = (dx * dx + dy * dy) + dz * dz;
-                                if (__builtin_amdgcn_ballot_w64(d2 < thr) != 0) {  // wave-uniform
-                                    ++n_acc;
-                                    insert<KMAX>(bd, bp, d2, (int)__double_as_longlong(c.w));  // no-op where d2 >= thr
-                                    thr = dmin(bd[KMAX - 1], ub2);
-                                    thrf = f32_bound(thr, cpass);
-                                }
-                            }
-                        }
-                    }
-                    n_cand += (uint32_t)nc;
-                    wave_lds_sync();
-                    stamp(t_comp);
+                    if (nbuf > kCap - 64) flush();
                 }
             }
+            flush();
             // ---- exactness: lanes with k-th distance <= R are final ----
             const double worst = uniform(wave_max(bd[KMAX - 1]));  // inactive lanes hold -1
             if (worst <= R * R || R >= a.rall) break;
@@ -705,13 +798,13 @@ __global__ __launch_bounds__(256) void k_knn_interp(KnnKernelArgs a, const doubl
         if (dbg != nullptr && gw < dbg_cap && (threadIdx.x & 63) == (int)__builtin_ffsll((long long)__builtin_amdgcn_ballot_w64(true)) - 1) {
             unsigned long long *r = dbg + gw * kStampFields;
             r[0] = t_setup;
-            r[1] = t_rows;
-            r[2] = t_copy;
-            r[3] = t_comp;
-            r[4] = t_epi;
-            r[5] = n_cand;
-            r[6] = n_acc;
-            r[7] = n_round + ((unsigned long long)n_pass << 32);
+            r[1] = t_seed;
+            r[2] = t_rows;
+            r[3] = t_copy;
+            r[4] = t_comp;
+            r[5] = t_epi;
+            r[6] = n_cand + ((unsigned long long)n_acc << 32);
+            r[7] = (n_round & 0xffffu) + ((unsigned long long)(n_pass & 0xffffu) << 16) + ((unsigned long long)n_surv << 32);
         }
     }
 }
