@@ -173,7 +173,6 @@ namespace {
 constexpr double kDefaultOccupancy = 1.2;  // particles per binning cell
 constexpr double kDefaultR0Scale = 1.0;     // first gather radius / expected k-NN radius
 constexpr long long kMaxCells = 1LL << 28;
-constexpr int kLatticeStep = 4;                 // coarse lattice = every 4th grid point (+ last)
 constexpr long long kLatticeStopPoints = 50000; // no coarser lattice below this many points
 
 int validate(const ptv_particles *p, const ptv_grid *g, const ptv_knn_params *prm) {
@@ -412,7 +411,6 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
         ll.cb.dk = lat[l + 1].dk;
         ll.cb.slots = lat[l + 1].slots;
         for (int d = 0; d < 3; ++d) ll.cb.n[d] = lat[l + 1].n[d];
-        ll.cb.step = kLatticeStep;
         PTV_TRY(launch_knn(ll, b, lat[l].ax, lat[l].ay, lat[l].az, nullptr, nullptr, nullptr, nullptr, lat[l].dk,
                            lat[l].dk, lat[l].dk, s));
     }
@@ -423,7 +421,6 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
         kl.cb.dk = lat[0].dk;
         kl.cb.slots = lat[0].slots;
         for (int d = 0; d < 3; ++d) kl.cb.n[d] = lat[0].n[d];
-        kl.cb.step = kLatticeStep;
     }
     PTV_HIP(hipEventRecord(c->ev_lat1, s));
     PTV_TRY(launch_knn(kl, b, ax, ay, az, qx, qy, qz, mask, U, V, W, s));

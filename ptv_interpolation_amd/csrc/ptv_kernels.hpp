@@ -24,12 +24,14 @@ size_t scan_partials_needed(size_t m);
 // Exact k-th-neighbour distances on a coarser separable lattice (every `step`-th
 // point of this launch's grid, plus the last): d_k(v) <= dk(c) + |v - c| for any
 // lattice point c bounds every voxel's search radius (triangle inequality).
+constexpr int kLatticeShift = 2;  // coarse lattice = every (1 << kLatticeShift)-th grid point (+ last)
+constexpr int kLatticeStep = 1 << kLatticeShift;
+
 struct CoarseBound {
     const double *ax = nullptr, *ay = nullptr, *az = nullptr;  // lattice axes
     const double *dk = nullptr;                                // (n[2], n[1], n[0]) k-th distances
     const uint32_t *slots = nullptr;  // (n[2], n[1], n[0], k) k-NN particle slots, or NULL (count bound)
     int n[3] = {0, 0, 0};
-    int step = 4;
 };
 
 constexpr int kModeInterp = 0;  // write U, V, W

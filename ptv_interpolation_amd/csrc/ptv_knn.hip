@@ -294,13 +294,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
         qz = qpz[vfull];
     }
     const bool active = (valid || a.point_per_wave) && (mask == nullptr || mask[vfull] != 0);
+    // seed slots (k-NN lists of the tile's 8 lattice corners: lane = corner * 8 + entry), issued
+    // first so that their latency overlaps the lattice-bound loads below
+    uint32_t seed_sl = 0xffffffffu;
+    if constexpr (KMAX <= 8) {
+        if (a.cb.slots != nullptr && !a.point_per_wave) {
+            const int jx0 = __builtin_amdgcn_readfirstlane(cx >> kLatticeShift);
+            const int jy0 = __builtin_amdgcn_readfirstlane(cy >> kLatticeShift);
+            const int jz0 = __builtin_amdgcn_readfirstlane((cz - a.z0) >> kLatticeShift);
+            const int cc = lane >> 3, j = lane & 7;
+            const int jx = min(jx0 + (cc & 1), a.cb.n[0] - 1);
+            const int jy = min(jy0 + ((cc >> 1) & 1), a.cb.n[1] - 1);
+            const int jz = min(jz0 + (cc >> 2), a.cb.n[2] - 1);
+            if (j < a.k) seed_sl = a.cb.slots[(((size_t)jz * a.cb.n[1] + jy) * a.cb.n[0] + jx) * a.k + j];
+        }
+    }
 
     // upper bound on this voxel's k-th distance from the coarse lattice (triangle inequality)
     double ub = INFINITY;
     if (a.cb.dk != nullptr && active) {
         // |v - c| in fp32 from lattice-relative offsets, rounded up: any upper bound is valid
-        const int st = a.cb.step;
-        const int j0[3] = {cx / st, cy / st, (cz - a.z0) / st};
+        const int j0[3] = {cx >> kLatticeShift, cy >> kLatticeShift, (cz - a.z0) >> kLatticeShift};
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
             const int jx = min(j0[0] + (c & 1), a.cb.n[0] - 1);
@@ -348,28 +362,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
                 //      k-th smallest distance to their (deduplicated) union bounds its k-th
                 //      neighbour distance from above, usually to within a few ulps, so the gather
                 //      radius is tight and one pass is exact. ----
-                const int st = a.cb.step;
-                const int jx0 = __builtin_amdgcn_readfirstlane(cx / st);
-                const int jy0 = __builtin_amdgcn_readfirstlane(cy / st);
-                const int jz0 = __builtin_amdgcn_readfirstlane((cz - a.z0) / st);
-                const int cc = lane >> 3, j = lane & 7;
-                const int jx = min(jx0 + (cc & 1), a.cb.n[0] - 1);
-                const int jy = min(jy0 + ((cc >> 1) & 1), a.cb.n[1] - 1);
-                const int jz = min(jz0 + (cc >> 2), a.cb.n[2] - 1);
-                uint32_t sl = 0xffffffffu;
-                if (j < a.k) sl = a.cb.slots[(((size_t)jz * a.cb.n[1] + jy) * a.cb.n[0] + jx) * a.k + j];
-                // bitonic sort of the 64 slots across the wave, then keep first occurrences
-#pragma unroll
-                for (int size = 2; size <= 64; size <<= 1) {
-#pragma unroll
-                    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-                        const uint32_t o = (uint32_t)__shfl_xor((int)sl, stride, 64);
-                        const bool keep_min = ((lane & stride) == 0) == ((lane & size) == 0);
-                        sl = keep_min ? min(sl, o) : max(sl, o);
-                    }
-                }
-                const uint32_t prv = (uint32_t)__shfl_up((int)sl, 1, 64);
-                const bool uniq = sl != 0xffffffffu && (lane == 0 || sl != prv);
+                // deduplicate through an LDS hash table (the candidate buffer, unused yet): every
+                // lane writes its id at its slot's hash and keeps the slot if its own id is read
+                // back.  Equal slots -> one survivor; distinct slots that collide -> one survivor
+                // too, which only drops a seed: any subset of k distinct particles still bounds.
+                uint32_t *tab = reinterpret_cast<uint32_t *>(buf);
+                const uint32_t sl = seed_sl;
+                const bool has = sl != 0xffffffffu;
+                const uint32_t hsh = (sl * 2654435761u) >> 22;  // 1024 entries = the 4 KB buffer
+                if (has) tab[hsh] = (uint32_t)lane;
+                wave_lds_sync();
+                const bool uniq = has && tab[hsh] == (uint32_t)lane;
                 const unsigned long long um = __builtin_amdgcn_ballot_w64(uniq);
                 const int nu = __builtin_popcountll(um);
                 const int pos = __builtin_amdgcn_mbcnt_hi((unsigned)(um >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)um, 0u));
