@@ -65,7 +65,7 @@ struct ptv_ctx {
     DevBuf<double> bbox_part, bbox_out;
     DevBuf<unsigned long long> dbg;
     DevBuf<double> lat_axes[kMaxLattice], lat_dk[kMaxLattice];  // coarse-lattice bound levels
-    DevBuf<uint32_t> lat_slots[kMaxLattice];                     // their k-NN lists (seeds)
+    DevBuf<double4> lat_recs[kMaxLattice];                       // their k-NN records (seeds)
     double *h_bbox = nullptr;  // pinned, 6 doubles
     ptv_stats last{};
 };
@@ -154,7 +154,7 @@ int ptv_free(ptv_ctx *c) {
     c->dbg.release();
     for (auto &b : c->lat_axes) b.release();
     for (auto &b : c->lat_dk) b.release();
-    for (auto &b : c->lat_slots) b.release();
+    for (auto &b : c->lat_recs) b.release();
     if (c->h_bbox) hipHostFree(c->h_bbox);
     hipEventDestroy(c->ev_knn0);
     hipEventDestroy(c->ev_knn1);
@@ -341,7 +341,7 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
     struct Lat {
         int n[3];
         double *ax, *ay, *az, *dk;
-        uint32_t *slots;  // NULL on the coarsest (count-bound) level
+        double4 *recs;  // NULL on the coarsest (count-bound) level and for k > 8
     };
     Lat lat[kMaxLattice];
     int nlat = 0;
@@ -359,7 +359,7 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
             L.ay = L.ax + L.n[0];
             L.az = L.ay + L.n[1];
             L.dk = c->lat_dk[nlat].p;
-            L.slots = nullptr;
+            L.recs = nullptr;
             double *dst[3] = {L.ax, L.ay, L.az};
             for (int d = 0; d < 3; ++d) PTV_TRY(launch_subsample(src[d], n[d], kLatticeStep, dst[d], L.n[d], s));
             for (int d = 0; d < 3; ++d) {
@@ -394,10 +394,12 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
                                        lat[l].n[2], prm->k, kl.r0, lat[l].dk, s));
             continue;
         }
-        PTV_TRY(c->lat_slots[l].ensure((size_t)lat[l].n[0] * lat[l].n[1] * lat[l].n[2] * prm->k));
-        lat[l].slots = c->lat_slots[l].p;
+        if (kmax_for(prm->k) <= 8) {  // seeds are used by the k <= 8 kernels only
+            PTV_TRY(c->lat_recs[l].ensure((size_t)lat[l].n[0] * lat[l].n[1] * lat[l].n[2] * prm->k));
+            lat[l].recs = c->lat_recs[l].p;
+        }
         KnnLaunch ll = kl;
-        ll.kd_slots = lat[l].slots;
+        ll.kd_recs = lat[l].recs;
         ll.nx = lat[l].n[0];
         ll.ny = lat[l].n[1];
         ll.nz = lat[l].n[2];
@@ -409,7 +411,7 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
         ll.cb.ay = lat[l + 1].ay;
         ll.cb.az = lat[l + 1].az;
         ll.cb.dk = lat[l + 1].dk;
-        ll.cb.slots = lat[l + 1].slots;
+        ll.cb.recs = lat[l + 1].recs;
         for (int d = 0; d < 3; ++d) ll.cb.n[d] = lat[l + 1].n[d];
         PTV_TRY(launch_knn(ll, b, lat[l].ax, lat[l].ay, lat[l].az, nullptr, nullptr, nullptr, nullptr, lat[l].dk,
                            lat[l].dk, lat[l].dk, s));
@@ -419,7 +421,7 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
         kl.cb.ay = lat[0].ay;
         kl.cb.az = lat[0].az;
         kl.cb.dk = lat[0].dk;
-        kl.cb.slots = lat[0].slots;
+        kl.cb.recs = lat[0].recs;
         for (int d = 0; d < 3; ++d) kl.cb.n[d] = lat[0].n[d];
     }
     PTV_HIP(hipEventRecord(c->ev_lat1, s));

@@ -30,7 +30,7 @@ constexpr int kLatticeStep = 1 << kLatticeShift;
 struct CoarseBound {
     const double *ax = nullptr, *ay = nullptr, *az = nullptr;  // lattice axes
     const double *dk = nullptr;                                // (n[2], n[1], n[0]) k-th distances
-    const uint32_t *slots = nullptr;  // (n[2], n[1], n[0], k) k-NN particle slots, or NULL (count bound)
+    const double4 *recs = nullptr;  // (n[2], n[1], n[0], k) k-NN particle records {x,y,z,slot}, or NULL
     int n[3] = {0, 0, 0};
 };
 
@@ -48,9 +48,8 @@ struct KnnLaunch {
     uint32_t flags;
     double r0;           // first gather radius (from the mean particle density)
     int mode = kModeInterp;
-    int point_per_wave = 0;  // 1: one grid point per wave (coarsest lattice)
     CoarseBound cb;
-    uint32_t *kd_slots = nullptr;  // kModeKDist: also write each point's k-NN slots here
+    double4 *kd_recs = nullptr;  // kModeKDist: also write each point's k-NN records here
 };
 
 // Upper bound on the k-th neighbour distance of every point of a separable grid by

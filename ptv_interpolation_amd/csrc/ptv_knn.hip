@@ -63,9 +63,8 @@ struct KnnKernelArgs {
     double r0;    // first gather radius
     double rall;  // radius that covers the whole cell grid from any query
     int mode;     // kModeInterp / kModeKDist
-    int point_per_wave;
     CoarseBound cb;
-    uint32_t *kd_slots;  // kModeKDist: k-NN slots out (NULL = none)
+    double4 *kd_recs;  // kModeKDist: k-NN particle records out (NULL = none)
 };
 
 // numpy pairwise sum of a[0..n) (n <= KMAX <= 128), from identity 0.0.
@@ -170,27 +169,22 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 template <int KMAX>
 __device__ __forceinline__ void insert(double (&bd)[KMAX], int (&bp)[KMAX], double d2, int p) {
-    // Descending sweep: slot j takes slot j-1 if the candidate beats j-1, else the candidate
-    // if it beats j, else keeps its value.  Written as bit-selects on all-ones/all-zeros
-    // masks so the compiler emits v_cmp + v_cndmask (no exec-mask branches).
-    const unsigned long long cu = (unsigned long long)__double_as_longlong(d2);
-    unsigned long long m_j = 0ull - (unsigned long long)(d2 < bd[KMAX - 1]);
+    // Ascending carry sweep: m_j = d2 < bd[j] is monotone in j over the sorted list; from the
+    // first j where it holds, slot j takes the carry (the candidate, then each displaced
+    // entry) and hands its old entry on.  Ties keep the earlier entry first.  Every slot is
+    // updated in place (selects on v_cmp masks, no exec-mask branches).
+    double cd = d2;
+    int cp = p;
 #pragma unroll
-    for (int j = KMAX - 1; j > 0; --j) {
-        const unsigned long long m_m = 0ull - (unsigned long long)(d2 < bd[j - 1]);
-        const unsigned long long cur = (unsigned long long)__double_as_longlong(bd[j]);
-        const unsigned long long prv = (unsigned long long)__double_as_longlong(bd[j - 1]);
-        unsigned long long t = (cur & ~m_j) | (cu & m_j);
-        t = (t & ~m_m) | (prv & m_m);
-        int ti = (bp[j] & ~(int)m_j) | (p & (int)m_j);
-        ti = (ti & ~(int)m_m) | (bp[j - 1] & (int)m_m);
-        bd[j] = __longlong_as_double((long long)t);
-        bp[j] = ti;
-        m_j = m_m;
+    for (int j = 0; j < KMAX; ++j) {
+        const bool mj = d2 < bd[j];
+        const double od = bd[j];
+        const int op = bp[j];
+        bd[j] = mj ? cd : od;
+        bp[j] = mj ? cp : op;
+        cd = mj ? od : cd;
+        cp = mj ? op : cp;
     }
-    const unsigned long long cur0 = (unsigned long long)__double_as_longlong(bd[0]);
-    bd[0] = __longlong_as_double((long long)((cur0 & ~m_j) | (cu & m_j)));
-    bp[0] = (bp[0] & ~(int)m_j) | (p & (int)m_j);
 }
 
 // min(a, b) for non-NaN operands without fmin's canonicalising v_max
@@ -209,8 +203,12 @@ __device__ __forceinline__ int clampi(double f, int n) {
 
 // an upper bound on sqrt(x), x >= 0, from the fp32 square root (any over-estimate of a
 // gather half-width only adds cells; the same inputs always give the same bound)
+__device__ __forceinline__ float sqrtf_up(float x) {  // x >= 0 already rounded up
+    // v_sqrt_f32 (1 ulp) with 8 ulps of slack; inputs below 1e-30 are raised to it
+    return __builtin_amdgcn_sqrtf(fmaxf(x, 1e-30f)) * 1.0000005f;
+}
 __device__ __forceinline__ double sqrt_up(double x) {
-    return (double)sqrtf((float)(x * (1.0 + 2.384185791015625e-07))) * (1.0 + 4.76837158203125e-07);
+    return (double)sqrtf_up((float)(x * (1.0 + 2.384185791015625e-07)));
 }
 
 // bijection of [0, nb): block b (dispatched to XCD b % 8) -> a contiguous range per XCD
@@ -260,27 +258,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
     // so give XCD x a contiguous range of tiles (neighbouring tiles share cell rows and
     // particle records; each XCD has its own L2)
     const int b = xcd_block(blockIdx.x, gridDim.x);
-    int ix, iy, iz;
-    if (a.point_per_wave) {
-        // every lane of the wave takes the same grid point (coarsest lattice: a point-sized
-        // box keeps each wave's candidate set small however sparse the lattice is)
-        const long long gp = (long long)b * 4 + wid;
-        if (gp >= (long long)a.nx * a.ny * (a.z1 - a.z0)) return;  // wave-uniform
-        ix = (int)(gp % a.nx);
-        iy = (int)((gp / a.nx) % a.ny);
-        iz = a.z0 + (int)(gp / ((long long)a.nx * a.ny));
-    } else {
-        const int bx = b % a.ntxb;
-        const int rr = b / a.ntxb;
-        const int ty = rr % a.nty;
-        const int tz = rr / a.nty;
-        const int tx = bx * 4 + wid;
-        if (tx >= a.ntx) return;  // wave-uniform
-        ix = tx * 4 + (lane & 3);
-        iy = ty * 4 + ((lane >> 2) & 3);
-        iz = a.z0 + tz * 4 + (lane >> 4);
-    }
-    const bool valid = ix < a.nx && iy < a.ny && iz < a.z1 && (!a.point_per_wave || lane == 0);
+    const int bx = b % a.ntxb;
+    const int rr = b / a.ntxb;
+    const int ty = rr % a.nty;
+    const int tz = rr / a.nty;
+    const int tx = bx * 4 + wid;
+    if (tx >= a.ntx) return;  // wave-uniform
+    const int ix = tx * 4 + (lane & 3);
+    const int iy = ty * 4 + ((lane >> 2) & 3);
+    const int iz = a.z0 + tz * 4 + (lane >> 4);
+    const bool valid = ix < a.nx && iy < a.ny && iz < a.z1;
     const int cx = min(ix, a.nx - 1), cy = min(iy, a.ny - 1), cz = min(iz, a.z1 - 1);
     const size_t vfull = ((size_t)cz * a.ny + cy) * a.nx + cx;
     double qx, qy, qz;
@@ -293,12 +280,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
         qy = qpy[vfull];
         qz = qpz[vfull];
     }
-    const bool active = (valid || a.point_per_wave) && (mask == nullptr || mask[vfull] != 0);
-    // seed slots (k-NN lists of the tile's 8 lattice corners: lane = corner * 8 + entry), issued
-    // first so that their latency overlaps the lattice-bound loads below
-    uint32_t seed_sl = 0xffffffffu;
+    const bool active = valid && (mask == nullptr || mask[vfull] != 0);
+    // seed records (k-NN lists of the tile's 8 lattice corners: lane = corner * 8 + entry, each a
+    // copy {x, y, z, slot} of the particle record), issued first so that their latency overlaps
+    // the lattice-bound loads below
+    double4 seed = make_double4(0.0, 0.0, 0.0, __longlong_as_double(-1LL));
     if constexpr (KMAX <= 8) {
-        if (a.cb.slots != nullptr && !a.point_per_wave) {
+        if (a.cb.recs != nullptr) {
             const int jx0 = __builtin_amdgcn_readfirstlane(cx >> kLatticeShift);
             const int jy0 = __builtin_amdgcn_readfirstlane(cy >> kLatticeShift);
             const int jz0 = __builtin_amdgcn_readfirstlane((cz - a.z0) >> kLatticeShift);
@@ -306,7 +294,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
             const int jx = min(jx0 + (cc & 1), a.cb.n[0] - 1);
             const int jy = min(jy0 + ((cc >> 1) & 1), a.cb.n[1] - 1);
             const int jz = min(jz0 + (cc >> 2), a.cb.n[2] - 1);
-            if (j < a.k) seed_sl = a.cb.slots[(((size_t)jz * a.cb.n[1] + jy) * a.cb.n[0] + jx) * a.k + j];
+            if (j < a.k) seed = a.cb.recs[(((size_t)jz * a.cb.n[1] + jy) * a.cb.n[0] + jx) * a.k + j];
         }
     }
 
@@ -314,7 +302,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
     double ub = INFINITY;
     if (a.cb.dk != nullptr && active) {
         // |v - c| in fp32 from lattice-relative offsets, rounded up: any upper bound is valid
-        const int j0[3] = {cx >> kLatticeShift, cy >> kLatticeShift, (cz - a.z0) >> kLatticeShift};
+        // the tile is one lattice cell: its corners are wave-uniform (scalar loads)
+        const int j0[3] = {__builtin_amdgcn_readfirstlane(cx >> kLatticeShift),
+                           __builtin_amdgcn_readfirstlane(cy >> kLatticeShift),
+                           __builtin_amdgcn_readfirstlane((cz - a.z0) >> kLatticeShift)};
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
             const int jx = min(j0[0] + (c & 1), a.cb.n[0] - 1);
@@ -323,7 +314,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
             const float ex = (float)(qx - a.cb.ax[jx]), ey = (float)(qy - a.cb.ay[jy]), ez = (float)(qz - a.cb.az[jz]);
             const float e2 = __fmaf_rn(ez, ez, __fmaf_rn(ey, ey, ex * ex));
             const double D = a.cb.dk[((size_t)jz * a.cb.n[1] + jy) * a.cb.n[0] + jx];
-            ub = fmin(ub, D + (double)(sqrtf(e2) * 1.000002f));
+            ub = fmin(ub, D + (double)(sqrtf_up(e2) * 1.000002f));
         }
         ub = ub * (1.0 + 1e-9) + a.cg.mg;
     }
@@ -346,18 +337,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
 
     stamp(t_setup);
     if (__builtin_amdgcn_ballot_w64(active) != 0) {
-        const double bx0 = uniform(wave_min(active ? qx : INFINITY)), bx1 = uniform(wave_max(active ? qx : -INFINITY));
-        const double by0 = uniform(wave_min(active ? qy : INFINITY)), by1 = uniform(wave_max(active ? qy : -INFINITY));
-        const double bz0 = uniform(wave_min(active ? qz : INFINITY)), bz1 = uniform(wave_max(active ? qz : -INFINITY));
+        // tile box (the gather geometry): on separable grids the extents of the tile's <= 4
+        // axis values (wave-uniform loads; padded and masked voxels only enlarge it), otherwise
+        // wave reductions over the active voxels
+        double bx0, bx1, by0, by1, bz0, bz1;
+        if (a.separable) {
+            auto ext = [](const double *axv, int i0, int imax, double &lo, double &hi) {
+                const double v0 = axv[i0], v1 = axv[min(i0 + 1, imax)], v2 = axv[min(i0 + 2, imax)],
+                             v3 = axv[min(i0 + 3, imax)];
+                lo = uniform(fmin(fmin(v0, v1), fmin(v2, v3)));
+                hi = uniform(fmax(fmax(v0, v1), fmax(v2, v3)));
+            };
+            ext(ax, tx * 4, a.nx - 1, bx0, bx1);
+            ext(ay, ty * 4, a.ny - 1, by0, by1);
+            ext(az, a.z0 + tz * 4, a.z1 - 1, bz0, bz1);
+        } else {
+            bx0 = uniform(wave_min(active ? qx : INFINITY));
+            bx1 = uniform(wave_max(active ? qx : -INFINITY));
+            by0 = uniform(wave_min(active ? qy : INFINITY));
+            by1 = uniform(wave_max(active ? qy : -INFINITY));
+            bz0 = uniform(wave_min(active ? qz : INFINITY));
+            bz1 = uniform(wave_max(active ? qz : -INFINITY));
+        }
         const CellGrid &g = a.cg;
         // tile centre: candidates and voxels get fp32 coordinates relative to it
         const double tcx = uniform(0.5 * (bx0 + bx1)), tcy = uniform(0.5 * (by0 + by1)), tcz = uniform(0.5 * (bz0 + bz1));
         const float qfx = (float)(qx - tcx), qfy = (float)(qy - tcy), qfz = (float)(qz - tcz);
         const f32x2 qf2x = {qfx, qfx}, qf2y = {qfy, qfy}, qf2z = {qfz, qfz};
-        const double bhalf = 0.5 * sqrt(((bx1 - bx0) * (bx1 - bx0) + (by1 - by0) * (by1 - by0)) + (bz1 - bz0) * (bz1 - bz0));
+        const double bhalf = 0.5 * sqrt_up(((bx1 - bx0) * (bx1 - bx0) + (by1 - by0) * (by1 - by0)) + (bz1 - bz0) * (bz1 - bz0));
         bool seeded = false;
         if constexpr (KMAX <= 8) {
-            if (a.cb.slots != nullptr && !a.point_per_wave) {
+            if (a.cb.recs != nullptr) {
                 // ---- seeds: the k-NN lists of the tile's 8 coarse-lattice corners.  Every lane's
                 //      k-th smallest distance to their (deduplicated) union bounds its k-th
                 //      neighbour distance from above, usually to within a few ulps, so the gather
@@ -367,8 +377,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
                 // back.  Equal slots -> one survivor; distinct slots that collide -> one survivor
                 // too, which only drops a seed: any subset of k distinct particles still bounds.
                 uint32_t *tab = reinterpret_cast<uint32_t *>(buf);
-                const uint32_t sl = seed_sl;
-                const bool has = sl != 0xffffffffu;
+                const uint32_t sl = (uint32_t)__double_as_longlong(seed.w);
+                const bool has = __double_as_longlong(seed.w) >= 0;
                 const uint32_t hsh = (sl * 2654435761u) >> 22;  // 1024 entries = the 4 KB buffer
                 if (has) tab[hsh] = (uint32_t)lane;
                 wave_lds_sync();
@@ -378,8 +388,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
                 const int pos = __builtin_amdgcn_mbcnt_hi((unsigned)(um >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)um, 0u));
                 double pm = 0.0;
                 if (uniq) {
-                    const double4 p4 = prec[sl];
-                    const double ex = p4.x - tcx, ey = p4.y - tcy, ez = p4.z - tcz;
+                    const double ex = seed.x - tcx, ey = seed.y - tcy, ez = seed.z - tcz;
                     fbx[pos] = (float)ex;
                     fby[pos] = (float)ey;
                     fbz[pos] = (float)ez;
@@ -416,7 +425,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
                     const double st2 = ((double)kth * (1.0 + 9.5367431640625e-07) + (2.0 * Ms * dl + dl * dl)) * (1.0 + 1e-12);
                     if (st2 < ub2) {
                         ub2 = st2;
-                        ub = sqrt(st2) * (1.0 + 1e-12);
+                        ub = sqrt_up(st2);
                     }
                 }
                 seeded = true;
@@ -440,9 +449,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
         //      every sub-ball can never enter any list (thresholds only shrink), so the copy drops it.
         //      fp32 on tile-relative coordinates, inflated for round-off (any over-estimate is safe).
         float sbx[2], sby[2], sbz[2], sbr2[8];  // sub-box s spans x-half s&1, y-half s>>1&1, z-half s>>2
-        double Mpass = 0.0;  // bound on |coordinate - tile centre| of this pass's candidates
-        auto subballs = [&]() {
-            float rv = thr < 0.0 ? -1.0f : sqrtf((float)(thr * (1.0 + 2.384185791015625e-07))) * 1.0000005f;
+        float sb_hd;                              // this lane's sub-box half-diagonal (rounded up)
+        {
             // extent of this lane's x-half (lanes agreeing in bit 1), y-half (bit 3), z-half (bit 5)
             float mnx = qfx, mxx = qfx, mny = qfy, mxy = qfy, mnz = qfz, mxz = qfz;
 #pragma unroll
@@ -459,12 +467,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
                     mnz = fminf(mnz, __shfl_xor(mnz, o, 64));
                     mxz = fmaxf(mxz, __shfl_xor(mxz, o, 64));
                 }
-                if (o == 1 || o == 4 || o == 16) rv = fmaxf(rv, __shfl_xor(rv, o, 64));
             }
             const float ux = mxx - mnx, uy = mxy - mny, uz = mxz - mnz;
-            const float hd = 0.5f * sqrtf(__fmaf_rn(uz, uz, __fmaf_rn(uy, uy, ux * ux))) * 1.00001f;
-            const float Rs = (rv + hd) * 1.00001f + (float)(Mpass * 1e-6);
-            const float R2s = rv < 0.0f ? -1.0f : Rs * Rs;
+            sb_hd = 0.5f * sqrtf_up(__fmaf_rn(uz, uz, __fmaf_rn(uy, uy, ux * ux)) * 1.000001f) * 1.00001f;
             const float cxs = 0.5f * (mnx + mxx), cys = 0.5f * (mny + mxy), czs = 0.5f * (mnz + mxz);
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
@@ -472,6 +477,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
                 sby[h] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cys), h << 3));
                 sbz[h] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(czs), h << 5));
             }
+        }
+        double Mpass = 0.0;  // bound on |coordinate - tile centre| of this pass's candidates
+        auto subballs = [&]() {
+            // radius of sub-ball s: max over its 8 lanes of sqrt(thr) + the half-diagonal
+            float rv = thr < 0.0 ? -1.0f : sqrtf_up((float)(thr * (1.0 + 2.384185791015625e-07)));
+#pragma unroll
+            for (int o = 1; o <= 16; o <<= 2) rv = fmaxf(rv, __shfl_xor(rv, o, 64));
+            const float Rs = (rv + sb_hd) * 1.00001f + (float)(Mpass * 1e-6);
+            const float R2s = rv < 0.0f ? -1.0f : Rs * Rs;
 #pragma unroll
             for (int sb = 0; sb < 8; ++sb) {
                 const int L = ((sb & 1) << 1) | ((sb & 2) << 2) | ((sb & 4) << 3);
@@ -488,10 +502,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
         auto flush = [&]() {
             if (nbuf == 0) return;
             wave_lds_sync();
-            for (int g0 = 0; g0 < nbuf; g0 += 32) {
-                const int ng = min(32, nbuf - g0);
+            for (int g0 = 0; g0 < nbuf; g0 += 64) {
+                const int ng = min(64, nbuf - g0);
                 // candidate g0 + j ends at bit nb - 1 - j (shift-in order keeps the loop rolled)
-                uint32_t m = 0u;
+                unsigned long long m = 0ull;
                 const int nb = (ng + 3) & ~3;
 #pragma unroll 1
                 for (int i0 = 0; i0 < ng; i0 += 4) {
@@ -512,24 +526,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
                                         ((s1.x <= thrf) ? 2u : 0u) | ((s1.y <= thrf) ? 1u : 0u);
                     m = (m << 4) | b4;
                 }
-                m &= ~((1u << (nb - ng)) - 1u);  // stale slots past nbuf
-                const double4 *gbuf = buf + g0 + nb - 32;  // bit position p <-> gbuf[31 - p]
-                while (__builtin_amdgcn_ballot_w64(m != 0u) != 0) {
+                m &= ~((1ull << (nb - ng)) - 1ull);  // stale slots past nbuf
+                const double4 *gbuf = buf + g0 + nb - 64;  // bit position p <-> gbuf[63 - p]
+                const int nit = __builtin_amdgcn_readfirstlane(wave_max_i(__builtin_popcountll(m)));
+                for (int it = 0; it < nit; ++it) {
+                    // branch-free body (lanes without bits read a valid stale slot and insert inf)
                     ++n_acc;
-                    double d2 = INFINITY;
-                    int slot = -1;
-                    if (m != 0u) {
-                        const int lz = __builtin_clz(m);
-                        m ^= 0x80000000u >> lz;
-                        const double4 c = gbuf[lz];
-                        const double dx = qx - c.x, dy = qy - c.y, dz = qz - c.z;
-                        const double e2 = (dx * dx + dy * dy) + dz * dz;
-                        if (e2 < thr) {
-                            d2 = e2;
-                            slot = (int)__double_as_longlong(c.w);
-                        }
-                    }
-                    insert<KMAX>(bd, bp, d2, slot);  // no-op where d2 = inf
+                    const bool has = m != 0ull;
+                    const int lz = __builtin_clzll(m | 1ull);
+                    m &= ~(0x8000000000000000ull >> lz);
+                    const double4 c = gbuf[lz];
+                    const double dx = qx - c.x, dy = qy - c.y, dz = qz - c.z;
+                    const double e2 = (dx * dx + dy * dy) + dz * dz;
+                    const double d2 = (has && e2 < thr) ? e2 : INFINITY;
+                    insert<KMAX>(bd, bp, d2, (int)__double_as_longlong(c.w));  // no-op where d2 = inf
                     thr = dmin(bd[KMAX - 1], ub2);
                 }
                 thrf = f32_bound(thr, cpass);
@@ -714,12 +724,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
     const size_t vo = ((size_t)(iz - a.z0) * a.ny + iy) * a.nx + ix;
     if (a.mode == kModeKDist) {
         U[vo] = sqrt(bd[KMAX - 1]);
-        if (a.kd_slots != nullptr) {
-            // the k-NN slots (list order) seed the next finer level's tiles
-            uint32_t *o = a.kd_slots + vo * (size_t)a.k;
+        if (a.kd_recs != nullptr) {
+            // the k-NN records (list order) seed the next finer level's tiles
+            double4 *o = a.kd_recs + vo * (size_t)a.k;
 #pragma unroll
-            for (int j = 0; j < KMAX; ++j)
-                if (j >= a.kpad) o[j - a.kpad] = (uint32_t)bp[j];
+            for (int j = 0; j < KMAX; ++j) {
+                if (j >= a.kpad) {
+                    double4 r = make_double4(0.0, 0.0, 0.0, __longlong_as_double(-1LL));
+                    if (bp[j] >= 0) {
+                        r = prec[bp[j]];
+                        r.w = __longlong_as_double((long long)bp[j]);
+                    }
+                    o[j - a.kpad] = r;
+                }
+            }
         }
         return;
     }
@@ -958,18 +976,15 @@ int launch_knn(const KnnLaunch &a, const Binned &b, const double *ax, const doub
     ka.flags = a.flags;
     ka.r0 = a.r0;
     ka.mode = a.mode;
-    ka.point_per_wave = a.point_per_wave;
     ka.cb = a.cb;
-    ka.kd_slots = a.kd_slots;
+    ka.kd_recs = a.kd_recs;
     double diag2 = 0.0;
     for (int d = 0; d < 3; ++d) {
         const double e = a.cg.cs[d] * a.cg.nc[d];
         diag2 += e * e;
     }
     ka.rall = sqrt(diag2) * (1.0 + 1e-9) + a.cg.mg;
-    const long long nblocks = a.point_per_wave
-                                  ? ((long long)a.nx * a.ny * (a.z1 - a.z0) + 3) / 4
-                                  : (long long)ka.ntxb * ka.nty * ka.ntz;
+    const long long nblocks = (long long)ka.ntxb * ka.nty * ka.ntz;
     if (nblocks > 0x7fffffffLL) {
         set_error("grid too large for one launch");
         return PTV_E_ARG;
