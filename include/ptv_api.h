@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define PTV_API_VERSION 1
+#define PTV_API_VERSION 2
 
 /* error codes */
 #define PTV_OK 0
@@ -40,7 +40,17 @@ extern "C" {
 #define PTV_METHOD_SIBSON 1
 #define PTV_METHOD_NEAREST 2
 
-/* flags for ptv_knn_params.flags */
+/* local RBF kernels (scipy RBFInterpolator names, _rbfinterp.py:19-28) */
+#define PTV_RBF_LINEAR 0
+#define PTV_RBF_THIN_PLATE_SPLINE 1
+#define PTV_RBF_CUBIC 2
+#define PTV_RBF_QUINTIC 3
+#define PTV_RBF_MULTIQUADRIC 4
+#define PTV_RBF_INVERSE_MULTIQUADRIC 5
+#define PTV_RBF_INVERSE_QUADRATIC 6
+#define PTV_RBF_GAUSSIAN 7
+
+/* flags for ptv_knn_params.flags / ptv_rbf_params.flags */
 #define PTV_FLAG_NAN_TO_NUM 1u  /* fused main.py:195-199 nan_to_num on the outputs */
 
 typedef struct ptv_ctx ptv_ctx;
@@ -91,6 +101,25 @@ typedef struct {
     int lattice_bounds;    /* >=0: coarse-lattice k-th distance bounds (default), <0: off */
 } ptv_knn_params;
 
+/*
+ * Local RBF parameters (interpolate_field rbf kwargs, interpolator.py:162-167, and the
+ * RBFInterpolator constructor they feed, _rbfinterp.py:258-345).  The caller resolves
+ * scipy's defaults and validation first (ptv_interpolation_amd/rbf.py): k is
+ * min(neighbors, n) (:322), epsilon is 1.0 for the scale-invariant kernels (:300-309),
+ * degree defaults to max(min_degree, 0) (:311-313).
+ */
+typedef struct {
+    int k;                /* rbf_neighbors, 1 <= k <= n */
+    int kernel;           /* PTV_RBF_* */
+    double epsilon;       /* shape parameter */
+    int degree;           /* polynomial degree, -1 = no polynomial; k + C(degree+3, 3) <= 64 */
+    double smoothing;     /* scalar smoothing, used when smoothing_per_point is NULL */
+    const double *smoothing_per_point; /* optional (n,) array, same memory space as the particles */
+    const uint8_t *fluid_mask;        /* as ptv_knn_params.fluid_mask */
+    uint32_t flags;       /* PTV_FLAG_* */
+    int chunk_planes;     /* z planes per k-NN + solve chunk (multiple of 4), <= 0: automatic */
+} ptv_rbf_params;
+
 /* Per-call timings (ms, hipEvent based) and sizes. */
 typedef struct {
     double ms_h2d, ms_bin, ms_lattice, ms_knn, ms_d2h, ms_total;
@@ -98,12 +127,14 @@ typedef struct {
     int32_t cells[3];
     double cell_size[3];
     double r0;
+    double ms_solve;     /* local RBF: the per-voxel solve kernels (ms_knn = their k-NN passes) */
+    int64_t n_singular;  /* local RBF: voxels whose system had an exactly zero pivot */
 } ptv_stats;
 
 /* Library / device management. */
 int ptv_version(void);
-/* sizeof(ptv_particles, ptv_grid, ptv_knn_params, ptv_stats): binding self-check */
-int ptv_abi_sizes(int64_t out4[4]);
+/* sizeof(ptv_particles, ptv_grid, ptv_knn_params, ptv_stats, ptv_rbf_params): binding self-check */
+int ptv_abi_sizes(int64_t out5[5]);
 const char *ptv_last_error(void);
 int ptv_device_count(int *out);
 int ptv_init(int device, ptv_ctx **out);
@@ -129,6 +160,26 @@ int ptv_interp_knn(ptv_ctx *ctx, const ptv_particles *p, const ptv_grid *g,
 int ptv_interp_knn_dev(ptv_ctx *ctx, const ptv_particles *p, const ptv_grid *g,
                        const ptv_knn_params *prm, double *U, double *V, double *W,
                        void *stream, ptv_stats *st);
+
+/*
+ * Local RBF interpolation, host buffers.
+ * Replaces the `method == 'rbf'` branch (interpolator.py:157-195) through scipy's
+ * RBFInterpolator(neighbors=k) evaluation (_rbfinterp.py:463-556): the KDTree build and
+ * query (:345, :513), the sort of each neighbourhood (:521), the per-neighbourhood
+ * system build (_build_system) and dgesv solve (:82-127), and the evaluation
+ * (_build_evaluation_coefficients @ coeffs, :384-418).  A system with an exactly zero
+ * pivot returns PTV_E_SINGULAR (scipy: LinAlgError "Singular matrix.", :115-127);
+ * the outputs are then undefined.
+ */
+int ptv_interp_rbf_local(ptv_ctx *ctx, const ptv_particles *p, const ptv_grid *g,
+                         const ptv_rbf_params *prm, double *U, double *V, double *W,
+                         ptv_stats *st);
+
+/* Same on device pointers; enqueued on `stream`, but synchronises once at the end to
+ * read the singular-system count (the return code depends on it). */
+int ptv_interp_rbf_local_dev(ptv_ctx *ctx, const ptv_particles *p, const ptv_grid *g,
+                             const ptv_rbf_params *prm, double *U, double *V, double *W,
+                             void *stream, ptv_stats *st);
 
 /*
  * Last-launch k-NN kernel duration in ms (hipEvent pair recorded around the

@@ -9,6 +9,10 @@ What it restates (reference = tombultreys/ptv_interpolation, read-only):
 
 * ``interpolator.interpolate_field`` IDW branch  (interpolator.py:126-155)
 * ``interpolator.interpolate_field`` Sibson branch (interpolator.py:83-124)
+* ``interpolator.interpolate_field`` local-RBF branch (interpolator.py:157-195)
+  through scipy's ``RBFInterpolator(neighbors=k)`` evaluation
+  (``_rbfinterp.py:463-556``, ``_build_system`` / ``dgesv`` :82-127): see
+  ``rbf_local_points`` below
 * the RBF process fan-out pattern (interpolator.py:173-182,
   test_parallel.py:6-28) as a z-slab ``ProcessPoolExecutor`` driver used as the
   same-box CPU baseline.
@@ -187,6 +191,114 @@ def interp_grid(points, values, ax, ay, az, method="idw", k=8, power=2.0, z0=0, 
     z1 = len(az) if z1 is None else z1
     q = grid_queries(ax, ay, az, z0, z1)
     out = interp_points(points, values, q, method, k, power, knn)
+    shape = (z1 - z0, len(ay), len(ax))
+    return tuple(np.ascontiguousarray(out[:, c].reshape(shape)) for c in range(3))
+
+
+# ----------------------------------------------------------------------------
+# local RBF (interpolator.py:157-195 -> scipy RBFInterpolator(neighbors=k))
+# ----------------------------------------------------------------------------
+# scipy/interpolate/_rbfinterp_pythran.py kernel functions of r = ||eps*x - eps*y||
+RBF_PHI = {
+    "linear": lambda r: -r,
+    "thin_plate_spline": lambda r: np.where(r == 0.0, 0.0, r * r * np.log(np.where(r == 0.0, 1.0, r))),
+    "cubic": lambda r: r * r * r,
+    "quintic": lambda r: -(r * r * r * r * r),
+    "multiquadric": lambda r: -np.sqrt(r * r + 1.0),
+    "inverse_multiquadric": lambda r: 1.0 / np.sqrt(r * r + 1.0),
+    "inverse_quadratic": lambda r: 1.0 / (r * r + 1.0),
+    "gaussian": lambda r: np.exp(-(r * r)),
+}
+RBF_SCALE_INVARIANT = {"linear", "thin_plate_spline", "cubic", "quintic"}
+RBF_MIN_DEGREE = {"multiquadric": 0, "linear": 0, "thin_plate_spline": 1, "cubic": 1, "quintic": 2}
+
+
+def monomial_powers(degree: int, ndim: int = 3) -> np.ndarray:
+    """_rbfinterp.py ``_monomial_powers``: exponents in combinations_with_replacement order."""
+    from itertools import combinations_with_replacement
+
+    rows = []
+    for deg in range(degree + 1):
+        for mono in combinations_with_replacement(range(ndim), deg):
+            r = [0] * ndim
+            for v in mono:
+                r[v] += 1
+            rows.append(r)
+    return np.array(rows, dtype=np.int64).reshape(-1, ndim)
+
+
+def _poly(xhat, powers):
+    """(..., 3) -> (..., R): prod over axes of xhat ** powers[j] (``_polynomial_matrix``)."""
+    return np.prod(xhat[..., None, :] ** powers, axis=-1)
+
+
+def rbf_local_points(points, values, queries, k, kernel="thin_plate_spline", epsilon=None, degree=None,
+                     smoothing=0.0, chunk=2048):
+    """RBFInterpolator(points, values, neighbors=k, kernel, epsilon, degree, smoothing)(queries).
+
+    Per query: KDTree k nearest (``_rbfinterp.py:513``), indices sorted ascending
+    (:521), system built per ``_build_system`` -- kernel block
+    ``phi(||eps*y_i - eps*y_j||)`` + smoothing on the diagonal, polynomial block
+    ``P((y - shift)/scale)`` with shift = (max+min)/2, scale = (max-min)/2 (0 -> 1)
+    over the neighbourhood -- solved with LAPACK gesv (numpy batched solve, the same
+    dgesv scipy calls at :113), evaluated as ``[phi(||eps*x - eps*y_j||), P((x -
+    shift)/scale)] @ coeffs`` (:404-418).  scipy solves each *unique* neighbourhood
+    once; solving it once per query gives the same coefficients.
+    Returns (Q, S) float64.  Singular systems raise numpy.linalg.LinAlgError.
+    """
+    from scipy.spatial import KDTree
+
+    y = np.asarray(points, dtype=np.float64)
+    d = np.asarray(values, dtype=np.float64).reshape(len(y), -1)
+    x = np.asarray(queries, dtype=np.float64).reshape(-1, 3)
+    if epsilon is None:
+        if kernel not in RBF_SCALE_INVARIANT:
+            raise ValueError("`epsilon` must be specified if `kernel` is not one of scale-invariant kernels.")
+        epsilon = 1.0
+    if degree is None:
+        degree = max(RBF_MIN_DEGREE.get(kernel, -1), 0)
+    powers = monomial_powers(degree)
+    k = int(min(k, len(y)))
+    sm = np.broadcast_to(np.asarray(smoothing, dtype=np.float64), (len(y),))
+    phi = RBF_PHI[kernel]
+    R = powers.shape[0]
+    m = k + R
+    _, idx = KDTree(y).query(x, k)
+    idx = np.sort(np.asarray(idx).reshape(len(x), k), axis=1)
+    out = np.empty((len(x), d.shape[1]))
+    for c0 in range(0, len(x), chunk):
+        ii = idx[c0:c0 + chunk]
+        yn = y[ii]  # (C, k, 3)
+        mins, maxs = yn.min(axis=1), yn.max(axis=1)
+        shift = (maxs + mins) / 2
+        scale = (maxs - mins) / 2
+        scale[scale == 0.0] = 1.0
+        ye = yn * epsilon
+        diff = ye[:, :, None, :] - ye[:, None, :, :]
+        r = np.sqrt((diff[..., 0] ** 2 + diff[..., 1] ** 2) + diff[..., 2] ** 2)
+        lhs = np.zeros((len(ii), m, m))
+        lhs[:, :k, :k] = phi(r)
+        lhs[:, np.arange(k), np.arange(k)] += sm[ii]
+        P = _poly((yn - shift[:, None, :]) / scale[:, None, :], powers)
+        lhs[:, :k, k:] = P
+        lhs[:, k:, :k] = np.swapaxes(P, 1, 2)
+        rhs = np.zeros((len(ii), m, d.shape[1]))
+        rhs[:, :k] = d[ii]
+        coeffs = np.linalg.solve(lhs, rhs)
+        xq = x[c0:c0 + chunk]
+        dq = xq[:, None, :] * epsilon - ye
+        rq = np.sqrt((dq[..., 0] ** 2 + dq[..., 1] ** 2) + dq[..., 2] ** 2)
+        vec = np.concatenate([phi(rq), _poly((xq - shift) / scale, powers)], axis=1)
+        out[c0:c0 + chunk] = np.einsum("qm,qms->qs", vec, coeffs)
+    return out
+
+
+def rbf_local_grid(points, values, ax, ay, az, k, kernel="thin_plate_spline", epsilon=None, degree=None,
+                   smoothing=0.0, z0=0, z1=None):
+    """Whole-grid (or z-slab) local RBF -> (U, V, W) each (nz', ny, nx)."""
+    z1 = len(az) if z1 is None else z1
+    q = grid_queries(ax, ay, az, z0, z1)
+    out = rbf_local_points(points, values, q, k, kernel, epsilon, degree, smoothing)
     shape = (z1 - z0, len(ay), len(ax))
     return tuple(np.ascontiguousarray(out[:, c].reshape(shape)) for c in range(3))
 

@@ -29,6 +29,18 @@ METHOD_NEAREST = 2
 
 FLAG_NAN_TO_NUM = 1
 
+# local RBF kernels (include/ptv_api.h PTV_RBF_*), scipy names
+RBF_KERNELS = {
+    "linear": 0,
+    "thin_plate_spline": 1,
+    "cubic": 2,
+    "quintic": 3,
+    "multiquadric": 4,
+    "inverse_multiquadric": 5,
+    "inverse_quadratic": 6,
+    "gaussian": 7,
+}
+
 _dp = C.POINTER(C.c_double)
 
 
@@ -49,12 +61,18 @@ class KnnParams(C.Structure):
                 ("r0_scale", C.c_double), ("lattice_bounds", C.c_int)]
 
 
+class RbfParams(C.Structure):
+    _fields_ = [("k", C.c_int), ("kernel", C.c_int), ("epsilon", C.c_double), ("degree", C.c_int),
+                ("smoothing", C.c_double), ("smoothing_per_point", _dp), ("fluid_mask", C.POINTER(C.c_uint8)),
+                ("flags", C.c_uint32), ("chunk_planes", C.c_int)]
+
+
 class Stats(C.Structure):
     _fields_ = [("ms_h2d", C.c_double), ("ms_bin", C.c_double), ("ms_lattice", C.c_double), ("ms_knn", C.c_double),
                 ("ms_d2h", C.c_double),
                 ("ms_total", C.c_double), ("n_particles", C.c_int64), ("n_voxels", C.c_int64),
                 ("n_cells", C.c_int64), ("cells", C.c_int32 * 3), ("cell_size", C.c_double * 3),
-                ("r0", C.c_double)]
+                ("r0", C.c_double), ("ms_solve", C.c_double), ("n_singular", C.c_int64)]
 
     def as_dict(self):
         d = {f: getattr(self, f) for f, _ in self._fields_}
@@ -74,6 +92,10 @@ EXPORTS = {
                                  _dp, _dp, _dp, C.POINTER(Stats)]),
     "ptv_interp_knn_dev": (C.c_int, [C.c_void_p, C.POINTER(Particles), C.POINTER(Grid), C.POINTER(KnnParams),
                                      _dp, _dp, _dp, C.c_void_p, C.POINTER(Stats)]),
+    "ptv_interp_rbf_local": (C.c_int, [C.c_void_p, C.POINTER(Particles), C.POINTER(Grid), C.POINTER(RbfParams),
+                                       _dp, _dp, _dp, C.POINTER(Stats)]),
+    "ptv_interp_rbf_local_dev": (C.c_int, [C.c_void_p, C.POINTER(Particles), C.POINTER(Grid),
+                                           C.POINTER(RbfParams), _dp, _dp, _dp, C.c_void_p, C.POINTER(Stats)]),
     "ptv_last_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
     "ptv_debug_stamps": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_double)]),
 }
@@ -116,15 +138,17 @@ def check(rc):
             raise MemoryError(msg)
         if rc == PTV_E_UNSUPPORTED:
             raise NotImplementedError(msg)
+        if rc == PTV_E_SINGULAR:
+            raise np.linalg.LinAlgError(msg)
         raise PtvError(rc, msg)
     return rc
 
 
 def abi_sizes():
     """(C sizeof, ctypes sizeof) for each ABI struct: they must agree."""
-    out = (C.c_int64 * 4)()
+    out = (C.c_int64 * 5)()
     check(lib().ptv_abi_sizes(out))
-    py = [C.sizeof(Particles), C.sizeof(Grid), C.sizeof(KnnParams), C.sizeof(Stats)]
+    py = [C.sizeof(Particles), C.sizeof(Grid), C.sizeof(KnnParams), C.sizeof(Stats), C.sizeof(RbfParams)]
     return list(out), py
 
 
@@ -218,6 +242,70 @@ class Context:
                                    as_dp(out[0]), as_dp(out[1]), as_dp(out[2]), C.byref(st)))
         self.stats = st.as_dict()
         return tuple(out)
+
+    def interp_rbf(self, points, values, axes=None, grid_points=None, shape=None, k=20,
+                   kernel="thin_plate_spline", epsilon=1.0, degree=1, smoothing=0.0, fluid_mask=None, flags=0,
+                   z_range=None, chunk_planes=0):
+        """Host-array local RBF (scipy RBFInterpolator(neighbors=k) semantics; the arguments are
+        already resolved by ptv_interpolation_amd.rbf).  ``smoothing``: scalar or (n,) array.
+        Returns (U, V, W) float64 (nz', ny, nx)."""
+        pts = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 3)
+        vals = np.ascontiguousarray(values, dtype=np.float64).reshape(-1, 3)
+        cols = [np.ascontiguousarray(pts[:, i]) for i in range(3)] + [np.ascontiguousarray(vals[:, i]) for i in range(3)]
+        P = Particles(pts.shape[0], *[as_dp(c) for c in cols])
+        keep = list(cols)
+        if axes is not None:
+            ax, ay, az = (np.ascontiguousarray(a, dtype=np.float64).ravel() for a in axes)
+            nx, ny, nz = len(ax), len(ay), len(az)
+            keep += [ax, ay, az]
+            G = Grid(nx, ny, nz, as_dp(ax), as_dp(ay), as_dp(az), None, None, None, 0, nz)
+        else:
+            nz, ny, nx = shape
+            gp = [np.ascontiguousarray(a, dtype=np.float64).ravel() for a in grid_points]
+            keep += gp
+            G = Grid(nx, ny, nz, None, None, None, as_dp(gp[0]), as_dp(gp[1]), as_dp(gp[2]), 0, nz)
+        z0, z1 = (0, nz) if z_range is None else z_range
+        G.z_begin, G.z_end = z0, z1
+        mk = None
+        if fluid_mask is not None:
+            mk = np.ascontiguousarray(fluid_mask, dtype=np.uint8).reshape(nz, ny, nx)
+            keep.append(mk)
+        sm_arr = None
+        if np.ndim(smoothing) > 0:
+            sm_arr = np.ascontiguousarray(smoothing, dtype=np.float64).ravel()
+            keep.append(sm_arr)
+        prm = RbfParams(int(k), RBF_KERNELS[kernel], float(epsilon), int(degree),
+                        0.0 if sm_arr is not None else float(smoothing),
+                        as_dp(sm_arr) if sm_arr is not None else None,
+                        mk.ctypes.data_as(C.POINTER(C.c_uint8)) if mk is not None else None, int(flags),
+                        int(chunk_planes))
+        out = [np.empty((z1 - z0, ny, nx), dtype=np.float64) for _ in range(3)]
+        st = Stats()
+        check(lib().ptv_interp_rbf_local(self.h, C.byref(P), C.byref(G), C.byref(prm),
+                                         as_dp(out[0]), as_dp(out[1]), as_dp(out[2]), C.byref(st)))
+        self.stats = st.as_dict()
+        return tuple(out)
+
+    def interp_rbf_dev(self, n, pptrs, nx, ny, nz, axes_ptrs=None, point_ptrs=None, out_ptrs=None, k=20,
+                       kernel="thin_plate_spline", epsilon=1.0, degree=1, smoothing=0.0, smoothing_ptr=0,
+                       mask_ptr=0, flags=0, z_range=None, stream=0, chunk_planes=0):
+        """Device-pointer local RBF (inputs resident in HBM); returns the call's stats."""
+        P = Particles(int(n), *[dev_dp(p) for p in pptrs])
+        if axes_ptrs is not None:
+            G = Grid(nx, ny, nz, *[dev_dp(p) for p in axes_ptrs], None, None, None, 0, nz)
+        else:
+            G = Grid(nx, ny, nz, None, None, None, *[dev_dp(p) for p in point_ptrs], 0, nz)
+        z0, z1 = (0, nz) if z_range is None else z_range
+        G.z_begin, G.z_end = z0, z1
+        prm = RbfParams(int(k), RBF_KERNELS[kernel], float(epsilon), int(degree), float(smoothing),
+                        dev_dp(smoothing_ptr) if smoothing_ptr else None,
+                        C.cast(C.c_void_p(mask_ptr), C.POINTER(C.c_uint8)) if mask_ptr else None, int(flags),
+                        int(chunk_planes))
+        st = Stats()
+        check(lib().ptv_interp_rbf_local_dev(self.h, C.byref(P), C.byref(G), C.byref(prm),
+                                             *[dev_dp(p) for p in out_ptrs], C.c_void_p(stream or 0),
+                                             C.byref(st)))
+        return st.as_dict()
 
     # -- device buffers (integer device pointers, e.g. torch tensor data_ptr()) --
     def interp_knn_dev(self, n, pptrs, nx, ny, nz, axes_ptrs=None, point_ptrs=None, out_ptrs=None,

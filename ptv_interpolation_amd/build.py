@@ -19,8 +19,11 @@ CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 LIB = os.path.join(HERE, "libptv_amd.so")
 BUILD = os.path.join(HERE, "csrc", "_build")
-SOURCES = ["ptv_api.cpp", "ptv_bin.hip", "ptv_knn.hip"]
+SOURCES = ["ptv_api.cpp", "ptv_bin.hip", "ptv_knn.hip", "ptv_rbf.hip"]
 ARCH = os.environ.get("PTV_OFFLOAD_ARCH", "gfx950")
+# per-file extras: the local-RBF kernel keeps each voxel's system row in registers, so every
+# loop over the row must unroll fully (a partial unroll turns the row into scratch memory)
+EXTRA = {"ptv_rbf.hip": ["-mllvm", "-pragma-unroll-threshold=1000000"]}
 
 COMMON = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", f"--offload-arch={ARCH}",
           "-I", INCLUDE, "-I", CSRC, "-Wno-unused-result"]
@@ -53,7 +56,7 @@ def build(verbose: bool = False, force: bool = False) -> str:
         objs.append(obj)
         if force or _stale(obj, [sp, __file__] + headers):
             lang = ["-x", "hip"] if src.endswith(".hip") else ["-x", "hip"]
-            jobs.append([cc, *COMMON, *lang, "-c", sp, "-o", obj])
+            jobs.append([cc, *COMMON, *EXTRA.get(src, []), *lang, "-c", sp, "-o", obj])
 
     def run(cmd):
         if verbose:

@@ -66,6 +66,11 @@ struct ptv_ctx {
     DevBuf<unsigned long long> dbg;
     DevBuf<double> lat_axes[kMaxLattice], lat_dk[kMaxLattice];  // coarse-lattice bound levels
     DevBuf<double4> lat_recs[kMaxLattice];                       // their k-NN records (seeds)
+    DevBuf<uint32_t> slots;                                      // local RBF: chunk k-NN slots
+    DevBuf<int> rbf_pw, rbf_status;                              // monomial exponents, singular count
+    DevBuf<double> smooth;                                       // per-particle smoothing (host calls)
+    std::vector<hipEvent_t> rbf_ev;                              // 3 per chunk: knn start, solve start, end
+    int rbf_chunks = 0;
     double *h_bbox = nullptr;  // pinned, 6 doubles
     ptv_stats last{};
 };
@@ -80,15 +85,16 @@ extern "C" {
 
 int ptv_version(void) { return PTV_API_VERSION; }
 
-int ptv_abi_sizes(int64_t out4[4]) {
-    if (!out4) {
+int ptv_abi_sizes(int64_t out5[5]) {
+    if (!out5) {
         set_error("ptv_abi_sizes: out is NULL");
         return PTV_E_ARG;
     }
-    out4[0] = (int64_t)sizeof(ptv_particles);
-    out4[1] = (int64_t)sizeof(ptv_grid);
-    out4[2] = (int64_t)sizeof(ptv_knn_params);
-    out4[3] = (int64_t)sizeof(ptv_stats);
+    out5[0] = (int64_t)sizeof(ptv_particles);
+    out5[1] = (int64_t)sizeof(ptv_grid);
+    out5[2] = (int64_t)sizeof(ptv_knn_params);
+    out5[3] = (int64_t)sizeof(ptv_stats);
+    out5[4] = (int64_t)sizeof(ptv_rbf_params);
     return PTV_OK;
 }
 
@@ -155,6 +161,11 @@ int ptv_free(ptv_ctx *c) {
     for (auto &b : c->lat_axes) b.release();
     for (auto &b : c->lat_dk) b.release();
     for (auto &b : c->lat_recs) b.release();
+    c->slots.release();
+    c->rbf_pw.release();
+    c->rbf_status.release();
+    c->smooth.release();
+    for (hipEvent_t e : c->rbf_ev) hipEventDestroy(e);
     if (c->h_bbox) hipHostFree(c->h_bbox);
     hipEventDestroy(c->ev_knn0);
     hipEventDestroy(c->ev_knn1);
@@ -175,7 +186,7 @@ constexpr double kDefaultR0Scale = 1.0;     // first gather radius / expected k-
 constexpr long long kMaxCells = 1LL << 28;
 constexpr long long kLatticeStopPoints = 50000; // no coarser lattice below this many points
 
-int validate(const ptv_particles *p, const ptv_grid *g, const ptv_knn_params *prm) {
+int validate(const ptv_particles *p, const ptv_grid *g, const void *prm) {
     if (!p || !g || !prm) {
         set_error("NULL particles/grid/params");
         return PTV_E_ARG;
@@ -202,6 +213,10 @@ int validate(const ptv_particles *p, const ptv_grid *g, const ptv_knn_params *pr
         set_error("grid: bad z slab [" + std::to_string(g->z_begin) + ", " + std::to_string(g->z_end) + ")");
         return PTV_E_ARG;
     }
+    return PTV_OK;
+}
+
+int validate_knn(const ptv_particles *p, const ptv_knn_params *prm) {
     if (prm->method != PTV_METHOD_IDW && prm->method != PTV_METHOD_SIBSON && prm->method != PTV_METHOD_NEAREST) {
         set_error("unknown method " + std::to_string(prm->method));
         return PTV_E_ARG;
@@ -279,9 +294,21 @@ double first_radius(const double lo[3], const double hi[3], int64_t n, int k, do
     return scale * std::pow((double)k * vol / ((double)n * unit), 1.0 / dims);
 }
 
-int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn_params *prm, const double *ax,
-            const double *ay, const double *az, const double *qx, const double *qy, const double *qz,
-            const uint8_t *mask, double *U, double *V, double *W, hipStream_t s, ptv_stats *st) {
+// Search settings shared by the k-NN consumers (IDW/Sibson epilogue, local RBF).
+struct SearchParams {
+    int method;  // PTV_METHOD_* (k-NN interpolation), ignored by the RBF path
+    int k;
+    double power, eps;
+    uint32_t flags;
+    double cell_occupancy, r0_scale;
+    int lattice_bounds;
+};
+
+// Steps 1-3 of every call: bounding box, binning, coarse-lattice k-th distance bounds.
+// Fills `kl` with a launch template for planes [z_begin, z_end) of the grid.
+int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchParams *prm, const double *ax,
+            const double *ay, const double *az, const double *qx, const double *qy, const double *qz, hipStream_t s,
+            KnnLaunch &kl, Binned &bout) {
     const int64_t n = p->n;
     const bool sep = ax != nullptr;
     const int64_t plane = g->nx * g->ny;
@@ -370,8 +397,7 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
         }
     }
 
-    // 4. k-NN interpolation
-    KnnLaunch kl;
+    // 4. launch template (k-NN search + consumer)
     kl.cg = cg;
     kl.nx = (int)g->nx;
     kl.ny = (int)g->ny;
@@ -386,6 +412,7 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
     kl.flags = prm->flags;
     kl.r0 = first_radius(lo, hi, n, prm->k, prm->r0_scale);
     Binned b{c->prec.p, c->pval.p, c->start.p, n};
+    bout = b;
     PTV_HIP(hipEventRecord(c->ev_knn0, s));
     for (int l = nlat - 1; l >= 0; --l) {  // coarsest first
         if (l == nlat - 1) {
@@ -425,9 +452,6 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
         for (int d = 0; d < 3; ++d) kl.cb.n[d] = lat[0].n[d];
     }
     PTV_HIP(hipEventRecord(c->ev_lat1, s));
-    PTV_TRY(launch_knn(kl, b, ax, ay, az, qx, qy, qz, mask, U, V, W, s));
-    PTV_HIP(hipEventRecord(c->ev_knn1, s));
-    c->timed_pending = true;
 
     ptv_stats &ls = c->last;
     ls = ptv_stats{};
@@ -439,16 +463,176 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
         ls.cell_size[a] = cg.cs[a];
     }
     ls.r0 = kl.r0;
-    if (st) *st = ls;
+    return PTV_OK;
+}
+
+SearchParams knn_search(const ptv_knn_params *prm) {
+    return SearchParams{prm->method, prm->k, prm->power, prm->eps, prm->flags, prm->cell_occupancy, prm->r0_scale,
+                        prm->lattice_bounds};
+}
+
+int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn_params *prm, const double *ax,
+            const double *ay, const double *az, const double *qx, const double *qy, const double *qz,
+            const uint8_t *mask, double *U, double *V, double *W, hipStream_t s, ptv_stats *st) {
+    const SearchParams sp = knn_search(prm);
+    KnnLaunch kl;
+    Binned b{};
+    PTV_TRY(prepare(c, p, g, &sp, ax, ay, az, qx, qy, qz, s, kl, b));
+    c->rbf_chunks = 0;
+    PTV_TRY(launch_knn(kl, b, ax, ay, az, qx, qy, qz, mask, U, V, W, s));
+    PTV_HIP(hipEventRecord(c->ev_knn1, s));
+    c->timed_pending = true;
+    if (st) *st = c->last;
+    return PTV_OK;
+}
+
+// monomial exponents of _monomial_powers(3, degree) (_rbfinterp.py:48-79), packed
+std::vector<int> monomial_powers(int degree) {
+    std::vector<int> out;
+    for (int d = 0; d <= degree; ++d) {
+        // combinations_with_replacement(range(3), d) in lexicographic order
+        std::vector<int> idx(d, 0);
+        while (true) {
+            int pw[3] = {0, 0, 0};
+            for (int v : idx) ++pw[v];
+            out.push_back(pw[0] | (pw[1] << 8) | (pw[2] << 16));
+            int i = d - 1;
+            while (i >= 0 && idx[i] == 2) --i;
+            if (i < 0) break;
+            ++idx[i];
+            for (int j = i + 1; j < d; ++j) idx[j] = idx[i];
+        }
+    }
+    return out;
+}
+
+int validate_rbf(const ptv_particles *p, const ptv_rbf_params *prm, int *m_out) {
+    if (prm->kernel < PTV_RBF_LINEAR || prm->kernel > PTV_RBF_GAUSSIAN) {
+        set_error("unknown RBF kernel " + std::to_string(prm->kernel));
+        return PTV_E_ARG;
+    }
+    if (prm->k < 1 || (int64_t)prm->k > p->n) {
+        set_error("k must be in [1, n]");
+        return PTV_E_ARG;
+    }
+    if (prm->degree < -1 || prm->degree > 8) {
+        set_error("degree must be in [-1, 8]");
+        return PTV_E_ARG;
+    }
+    if (!std::isfinite(prm->epsilon)) {
+        set_error("epsilon must be finite");
+        return PTV_E_ARG;
+    }
+    const int nm = (int)monomial_powers(prm->degree).size();
+    if (nm > prm->k) {
+        set_error("At least " + std::to_string(nm) + " data points are required when `degree` is " +
+                  std::to_string(prm->degree) + " and the number of dimensions is 3.");
+        return PTV_E_ARG;
+    }
+    const int m = prm->k + nm;
+    if (rbf_system_size(m) == 0 || kmax_for(prm->k) == 0) {
+        set_error("local RBF system of size " + std::to_string(m) + " (k=" + std::to_string(prm->k) +
+                  ") exceeds the GPU limit (" + std::to_string(kRbfMaxSystem) + ")");
+        return PTV_E_UNSUPPORTED;
+    }
+    *m_out = m;
+    return PTV_OK;
+}
+
+// Local RBF: per z chunk, a k-NN pass in slot mode, then the per-voxel solve.
+int run_rbf(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_rbf_params *prm, int m,
+            const double *ax, const double *ay, const double *az, const double *qx, const double *qy,
+            const double *qz, const double *smooth, const uint8_t *mask, double *U, double *V, double *W,
+            hipStream_t s, int64_t *n_singular) {
+    const SearchParams sp{PTV_METHOD_IDW, prm->k, 2.0, 1e-10, 0u, 0.0, 0.0, 0};
+    KnnLaunch kl;
+    Binned b{};
+    PTV_TRY(prepare(c, p, g, &sp, ax, ay, az, qx, qy, qz, s, kl, b));
+    const std::vector<int> pw = monomial_powers(prm->degree);
+    PTV_TRY(c->rbf_pw.ensure(pw.size() + 1));
+    PTV_TRY(c->rbf_status.ensure(2));
+    if (!pw.empty())
+        PTV_HIP(hipMemcpyAsync(c->rbf_pw.p, pw.data(), pw.size() * sizeof(int), hipMemcpyHostToDevice, s));
+    const int st_init[2] = {0, 0x7fffffff};
+    PTV_HIP(hipMemcpyAsync(c->rbf_status.p, st_init, sizeof(st_init), hipMemcpyHostToDevice, s));
+
+    const int64_t plane = g->nx * g->ny;
+    const int64_t z0 = g->z_begin, z1 = g->z_end;
+    int cp = prm->chunk_planes;
+    if (cp <= 0) {
+        // about 512 MB of slots per chunk
+        const int64_t per_plane = plane * (int64_t)prm->k * 4;
+        cp = (int)std::max<int64_t>(4, std::min<int64_t>(z1 - z0, ((int64_t)512 << 20) / std::max<int64_t>(per_plane, 1)));
+    }
+    cp = std::max(4, (cp + 3) & ~3);
+    PTV_TRY(c->slots.ensure((size_t)std::min<int64_t>(cp, z1 - z0) * plane * prm->k));
+    const int nchunks = (int)((z1 - z0 + cp - 1) / cp);
+    while ((int)c->rbf_ev.size() < 3 * nchunks) {
+        hipEvent_t e;
+        PTV_HIP(hipEventCreate(&e));
+        c->rbf_ev.push_back(e);
+    }
+    RbfKernelArgs ra{};
+    ra.nx = (int)g->nx;
+    ra.ny = (int)g->ny;
+    ra.out_z0 = (int)z0;
+    ra.separable = ax != nullptr ? 1 : 0;
+    ra.k = prm->k;
+    ra.m = m;
+    ra.kernel = prm->kernel;
+    ra.epsilon = prm->epsilon;
+    ra.smoothing = prm->smoothing;
+    ra.flags = prm->flags;
+    for (int ch = 0; ch < nchunks; ++ch) {
+        const int za = (int)(z0 + (int64_t)ch * cp), zb = (int)std::min<int64_t>(z1, za + cp);
+        KnnLaunch cl = kl;
+        cl.z0 = za;
+        cl.z1 = zb;
+        cl.lz0 = (int)z0;
+        cl.mode = kModeSlots;
+        cl.slots = c->slots.p;
+        PTV_HIP(hipEventRecord(c->rbf_ev[3 * ch], s));
+        PTV_TRY(launch_knn(cl, b, ax, ay, az, qx, qy, qz, mask, nullptr, nullptr, nullptr, s));
+        PTV_HIP(hipEventRecord(c->rbf_ev[3 * ch + 1], s));
+        ra.z0 = za;
+        ra.z1 = zb;
+        PTV_TRY(launch_rbf(ra, b, c->slots.p, ax, ay, az, qx, qy, qz, smooth, c->rbf_pw.p, mask, U, V, W,
+                           c->rbf_status.p, s));
+        PTV_HIP(hipEventRecord(c->rbf_ev[3 * ch + 2], s));
+    }
+    c->rbf_chunks = nchunks;
+    int st_out[2] = {0, 0};
+    PTV_HIP(hipMemcpyAsync(st_out, c->rbf_status.p, sizeof(st_out), hipMemcpyDeviceToHost, s));
+    PTV_HIP(hipStreamSynchronize(s));
+    *n_singular = st_out[0];
+    c->last.n_singular = st_out[0];
+    if (st_out[0] > 0) {
+        set_error("Singular matrix. (" + std::to_string(st_out[0]) + " voxel system(s), first at linear voxel " +
+                  std::to_string(st_out[1]) + ")");
+        return PTV_E_SINGULAR;
+    }
     return PTV_OK;
 }
 
 int finish_timing(ptv_ctx *c) {
     if (!c->timed_pending) return PTV_OK;
-    PTV_HIP(hipEventSynchronize(c->ev_knn1));
     float ms = 0.f;
-    PTV_HIP(hipEventElapsedTime(&ms, c->ev_lat1, c->ev_knn1));
-    c->last.ms_knn = ms;
+    if (c->rbf_chunks > 0) {
+        PTV_HIP(hipEventSynchronize(c->rbf_ev[3 * c->rbf_chunks - 1]));
+        double knn = 0.0, solve = 0.0;
+        for (int ch = 0; ch < c->rbf_chunks; ++ch) {
+            PTV_HIP(hipEventElapsedTime(&ms, c->rbf_ev[3 * ch], c->rbf_ev[3 * ch + 1]));
+            knn += ms;
+            PTV_HIP(hipEventElapsedTime(&ms, c->rbf_ev[3 * ch + 1], c->rbf_ev[3 * ch + 2]));
+            solve += ms;
+        }
+        c->last.ms_knn = knn;
+        c->last.ms_solve = solve;
+    } else {
+        PTV_HIP(hipEventSynchronize(c->ev_knn1));
+        PTV_HIP(hipEventElapsedTime(&ms, c->ev_lat1, c->ev_knn1));
+        c->last.ms_knn = ms;
+    }
     PTV_HIP(hipEventElapsedTime(&ms, c->ev_knn0, c->ev_lat1));
     c->last.ms_lattice = ms;
     PTV_HIP(hipEventElapsedTime(&ms, c->ev_bin0, c->ev_bin1));
@@ -457,52 +641,27 @@ int finish_timing(ptv_ctx *c) {
     return PTV_OK;
 }
 
-}  // namespace
+struct EventSet {
+    hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr};
+    ~EventSet() {
+        for (hipEvent_t x : e)
+            if (x) hipEventDestroy(x);
+    }
+};
 
-extern "C" {
-
-int ptv_interp_knn_dev(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn_params *prm, double *U,
-                       double *V, double *W, void *stream, ptv_stats *st) {
-    if (!c) {
-        set_error("NULL context");
-        return PTV_E_ARG;
-    }
-    PTV_TRY(validate(p, g, prm));
-    if (!U || !V || !W) {
-        set_error("NULL output");
-        return PTV_E_ARG;
-    }
-    PTV_HIP(hipSetDevice(c->device));
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    const bool sep = g->ax && g->ay && g->az;
-    return run_knn(c, p, g, prm, sep ? g->ax : nullptr, sep ? g->ay : nullptr, sep ? g->az : nullptr,
-                   sep ? nullptr : g->px, sep ? nullptr : g->py, sep ? nullptr : g->pz, prm->fluid_mask, U, V, W, s,
-                   st);
-}
-
-int ptv_interp_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn_params *prm, double *U,
-                   double *V, double *W, ptv_stats *st) {
-    if (!c) {
-        set_error("NULL context");
-        return PTV_E_ARG;
-    }
-    PTV_TRY(validate(p, g, prm));
-    if (!U || !V || !W) {
-        set_error("NULL output");
-        return PTV_E_ARG;
-    }
-    PTV_HIP(hipSetDevice(c->device));
+// Host-buffer call: H2D into the context's buffers, `compute` on device pointers, D2H of
+// the slab's three output planes, timings.  compute(dp, dg, dmask, dsmooth, U, V, W, s).
+template <typename F>
+int host_call(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const uint8_t *mask_h, const double *smooth_h,
+              double *U, double *V, double *W, F &&compute) {
     hipStream_t s = c->stream;
-    hipEvent_t t0, t1, t2;
-    PTV_HIP(hipEventCreate(&t0));
-    PTV_HIP(hipEventCreate(&t1));
-    PTV_HIP(hipEventCreate(&t2));
-    PTV_HIP(hipEventRecord(t0, s));
+    EventSet ev;
+    for (hipEvent_t &e : ev.e) PTV_HIP(hipEventCreate(&e));
+    PTV_HIP(hipEventRecord(ev.e[0], s));
     const int64_t n = p->n;
     const int64_t plane = g->nx * g->ny;
     const int64_t nvox = (g->z_end - g->z_begin) * plane;
     const int64_t nfull = g->nz * plane;
-    // H2D: particles
     const double *src[6] = {p->x, p->y, p->z, p->u, p->v, p->w};
     for (int i = 0; i < 6; ++i) {
         PTV_TRY(c->pin[i].ensure(n));
@@ -532,35 +691,111 @@ int ptv_interp_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const 
         dg.pz = c->qpts[2].p;
     }
     const uint8_t *dmask = nullptr;
-    if (prm->fluid_mask) {
+    if (mask_h) {
         PTV_TRY(c->mask.ensure(nfull));
-        PTV_HIP(hipMemcpyAsync(c->mask.p, prm->fluid_mask, nfull, hipMemcpyHostToDevice, s));
+        PTV_HIP(hipMemcpyAsync(c->mask.p, mask_h, nfull, hipMemcpyHostToDevice, s));
         dmask = c->mask.p;
     }
+    const double *dsmooth = nullptr;
+    if (smooth_h) {
+        PTV_TRY(c->smooth.ensure(n));
+        PTV_HIP(hipMemcpyAsync(c->smooth.p, smooth_h, n * sizeof(double), hipMemcpyHostToDevice, s));
+        dsmooth = c->smooth.p;
+    }
     for (int i = 0; i < 3; ++i) PTV_TRY(c->out[i].ensure(nvox));
-    PTV_HIP(hipEventRecord(t1, s));
-    PTV_TRY(run_knn(c, &dp, &dg, prm, dg.ax, dg.ay, dg.az, dg.px, dg.py, dg.pz, dmask, c->out[0].p, c->out[1].p,
-                    c->out[2].p, s, nullptr));
-    PTV_HIP(hipEventRecord(t2, s));
+    PTV_HIP(hipEventRecord(ev.e[1], s));
+    PTV_TRY(compute(&dp, &dg, dmask, dsmooth, c->out[0].p, c->out[1].p, c->out[2].p, s));
+    PTV_HIP(hipEventRecord(ev.e[2], s));
     double *dst[3] = {U, V, W};
     for (int i = 0; i < 3; ++i)
         PTV_HIP(hipMemcpyAsync(dst[i], c->out[i].p, nvox * sizeof(double), hipMemcpyDeviceToHost, s));
-    hipEvent_t t3;
-    PTV_HIP(hipEventCreate(&t3));
-    PTV_HIP(hipEventRecord(t3, s));
+    PTV_HIP(hipEventRecord(ev.e[3], s));
     PTV_HIP(hipStreamSynchronize(s));
     PTV_TRY(finish_timing(c));
     float h2d = 0.f, d2h = 0.f, tot = 0.f;
-    PTV_HIP(hipEventElapsedTime(&h2d, t0, t1));
-    PTV_HIP(hipEventElapsedTime(&d2h, t2, t3));
-    PTV_HIP(hipEventElapsedTime(&tot, t0, t3));
+    PTV_HIP(hipEventElapsedTime(&h2d, ev.e[0], ev.e[1]));
+    PTV_HIP(hipEventElapsedTime(&d2h, ev.e[2], ev.e[3]));
+    PTV_HIP(hipEventElapsedTime(&tot, ev.e[0], ev.e[3]));
     c->last.ms_h2d = h2d;
     c->last.ms_d2h = d2h;
     c->last.ms_total = tot;
-    hipEventDestroy(t0);
-    hipEventDestroy(t1);
-    hipEventDestroy(t2);
-    hipEventDestroy(t3);
+    return PTV_OK;
+}
+
+int check_call(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const void *prm, double *U, double *V,
+               double *W) {
+    if (!c) {
+        set_error("NULL context");
+        return PTV_E_ARG;
+    }
+    PTV_TRY(validate(p, g, prm));
+    if (!U || !V || !W) {
+        set_error("NULL output");
+        return PTV_E_ARG;
+    }
+    PTV_HIP(hipSetDevice(c->device));
+    return PTV_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ptv_interp_knn_dev(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn_params *prm, double *U,
+                       double *V, double *W, void *stream, ptv_stats *st) {
+    PTV_TRY(check_call(c, p, g, prm, U, V, W));
+    PTV_TRY(validate_knn(p, prm));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    const bool sep = g->ax && g->ay && g->az;
+    return run_knn(c, p, g, prm, sep ? g->ax : nullptr, sep ? g->ay : nullptr, sep ? g->az : nullptr,
+                   sep ? nullptr : g->px, sep ? nullptr : g->py, sep ? nullptr : g->pz, prm->fluid_mask, U, V, W, s,
+                   st);
+}
+
+int ptv_interp_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn_params *prm, double *U,
+                   double *V, double *W, ptv_stats *st) {
+    PTV_TRY(check_call(c, p, g, prm, U, V, W));
+    PTV_TRY(validate_knn(p, prm));
+    PTV_TRY(host_call(c, p, g, prm->fluid_mask, nullptr, U, V, W,
+                      [&](const ptv_particles *dp, const ptv_grid *dg, const uint8_t *dmask, const double *,
+                          double *dU, double *dV, double *dW, hipStream_t s) {
+                          return run_knn(c, dp, dg, prm, dg->ax, dg->ay, dg->az, dg->px, dg->py, dg->pz, dmask, dU,
+                                         dV, dW, s, nullptr);
+                      }));
+    if (st) *st = c->last;
+    return PTV_OK;
+}
+
+int ptv_interp_rbf_local_dev(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_rbf_params *prm,
+                             double *U, double *V, double *W, void *stream, ptv_stats *st) {
+    PTV_TRY(check_call(c, p, g, prm, U, V, W));
+    int m = 0;
+    PTV_TRY(validate_rbf(p, prm, &m));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    const bool sep = g->ax && g->ay && g->az;
+    int64_t nsing = 0;
+    const int rc = run_rbf(c, p, g, prm, m, sep ? g->ax : nullptr, sep ? g->ay : nullptr, sep ? g->az : nullptr,
+                           sep ? nullptr : g->px, sep ? nullptr : g->py, sep ? nullptr : g->pz,
+                           prm->smoothing_per_point, prm->fluid_mask, U, V, W, s, &nsing);
+    c->timed_pending = true;
+    if (st) *st = c->last;
+    return rc;
+}
+
+int ptv_interp_rbf_local(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_rbf_params *prm,
+                         double *U, double *V, double *W, ptv_stats *st) {
+    PTV_TRY(check_call(c, p, g, prm, U, V, W));
+    int m = 0;
+    PTV_TRY(validate_rbf(p, prm, &m));
+    PTV_TRY(host_call(c, p, g, prm->fluid_mask, prm->smoothing_per_point, U, V, W,
+                      [&](const ptv_particles *dp, const ptv_grid *dg, const uint8_t *dmask, const double *dsmooth,
+                          double *dU, double *dV, double *dW, hipStream_t s) {
+                          int64_t nsing = 0;
+                          const int rc = run_rbf(c, dp, dg, prm, m, dg->ax, dg->ay, dg->az, dg->px, dg->py, dg->pz,
+                                                 dsmooth, dmask, dU, dV, dW, s, &nsing);
+                          c->timed_pending = true;
+                          return rc;
+                      }));
     if (st) *st = c->last;
     return PTV_OK;
 }

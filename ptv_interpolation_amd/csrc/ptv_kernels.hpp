@@ -36,6 +36,7 @@ struct CoarseBound {
 
 constexpr int kModeInterp = 0;  // write U, V, W
 constexpr int kModeKDist = 1;   // write the exact k-th neighbour distance into U
+constexpr int kModeSlots = 2;   // write each voxel's k neighbour slots (sorted-record indices)
 
 struct KnnLaunch {
     CellGrid cg;
@@ -50,6 +51,8 @@ struct KnnLaunch {
     int mode = kModeInterp;
     CoarseBound cb;
     double4 *kd_recs = nullptr;  // kModeKDist: also write each point's k-NN records here
+    int lz0 = -1;                // plane of lattice point 0 (-1: z0); chunked launches keep the slab's
+    uint32_t *slots = nullptr;   // kModeSlots: (z1 - z0, ny, nx, k) neighbour slots out
 };
 
 // Upper bound on the k-th neighbour distance of every point of a separable grid by
@@ -67,5 +70,29 @@ extern long long g_dbg_cap;
 int launch_knn(const KnnLaunch &a, const Binned &b, const double *ax, const double *ay, const double *az,
                const double *qx, const double *qy, const double *qz, const uint8_t *mask, double *U, double *V,
                double *W, hipStream_t s);
+
+// ---- local RBF (ptv_rbf.hip) ----
+constexpr int kRbfMaxSystem = 64;  // k + #monomials per voxel system
+
+struct RbfKernelArgs {
+    int nx, ny;      // grid plane
+    int z0, z1;      // planes of this launch (chunk)
+    int out_z0;      // plane of output row 0 (the slab start)
+    int separable;
+    int k, m;        // neighbours, system size (k + #monomials)
+    int kernel;      // PTV_RBF_*
+    double epsilon;
+    double smoothing;  // scalar smoothing (when no per-particle array is given)
+    uint32_t flags;
+};
+
+int rbf_system_size(int m);  // padded system size served, 0 if unsupported
+
+// slots: (z1 - z0, ny, nx, k) neighbour slots from launch_knn(kModeSlots); pw: the
+// monomial exponents (m - k entries, px | py << 8 | pz << 16); status[0] counts singular
+// systems, status[1] keeps the lowest singular voxel index.
+int launch_rbf(const RbfKernelArgs &ka, const Binned &b, const uint32_t *slots, const double *ax, const double *ay,
+               const double *az, const double *qx, const double *qy, const double *qz, const double *smooth,
+               const int *pw, const uint8_t *mask, double *U, double *V, double *W, int *status, hipStream_t s);
 
 }  // namespace ptv

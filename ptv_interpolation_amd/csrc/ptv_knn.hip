@@ -65,6 +65,8 @@ struct KnnKernelArgs {
     int mode;     // kModeInterp / kModeKDist
     CoarseBound cb;
     double4 *kd_recs;  // kModeKDist: k-NN particle records out (NULL = none)
+    int lz0;           // plane of coarse-lattice point 0
+    uint32_t *slots;   // kModeSlots: neighbour slots out
 };
 
 // numpy pairwise sum of a[0..n) (n <= KMAX <= 128), from identity 0.0.
@@ -289,7 +291,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
         if (a.cb.recs != nullptr) {
             const int jx0 = __builtin_amdgcn_readfirstlane(cx >> kLatticeShift);
             const int jy0 = __builtin_amdgcn_readfirstlane(cy >> kLatticeShift);
-            const int jz0 = __builtin_amdgcn_readfirstlane((cz - a.z0) >> kLatticeShift);
+            const int jz0 = __builtin_amdgcn_readfirstlane((cz - a.lz0) >> kLatticeShift);
             const int cc = lane >> 3, j = lane & 7;
             const int jx = min(jx0 + (cc & 1), a.cb.n[0] - 1);
             const int jy = min(jy0 + ((cc >> 1) & 1), a.cb.n[1] - 1);
@@ -305,7 +307,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
         // the tile is one lattice cell: its corners are wave-uniform (scalar loads)
         const int j0[3] = {__builtin_amdgcn_readfirstlane(cx >> kLatticeShift),
                            __builtin_amdgcn_readfirstlane(cy >> kLatticeShift),
-                           __builtin_amdgcn_readfirstlane((cz - a.z0) >> kLatticeShift)};
+                           __builtin_amdgcn_readfirstlane((cz - a.lz0) >> kLatticeShift)};
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
             const int jx = min(j0[0] + (c & 1), a.cb.n[0] - 1);
@@ -741,6 +743,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
         }
         return;
     }
+    if (a.mode == kModeSlots) {
+        // the k neighbour slots (list order) for the local-RBF solve (ptv_rbf.hip)
+        if (!active) return;
+        uint32_t *o = a.slots + vo * (size_t)a.k;
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j)
+            if (j >= a.kpad) o[j - a.kpad] = (uint32_t)bp[j];
+        return;
+    }
     if (!active) {
         U[vo] = 0.0;
         V[vo] = 0.0;
@@ -978,6 +989,12 @@ int launch_knn(const KnnLaunch &a, const Binned &b, const double *ax, const doub
     ka.mode = a.mode;
     ka.cb = a.cb;
     ka.kd_recs = a.kd_recs;
+    ka.lz0 = a.lz0 < 0 ? a.z0 : a.lz0;
+    ka.slots = a.slots;
+    if (a.mode == kModeSlots && (a.slots == nullptr || (a.z0 - ka.lz0) % 4 != 0)) {
+        set_error("slot-mode k-NN launch needs an output buffer and a tile-aligned first plane");
+        return PTV_E_ARG;
+    }
     double diag2 = 0.0;
     for (int d = 0; d < 3; ++d) {
         const double e = a.cg.cs[d] * a.cg.nc[d];

@@ -207,7 +207,8 @@ def interpolate_field(df, grid_tuple, method="linear", rbf_neighbors=20, rbf_ker
               f"smoothing={smoothing} and n_jobs={n_jobs}...")
         from . import rbf as _rbf
 
-        return _rbf.rbf_field(points, values, grid_tuple, int(rbf_neighbors), rbf_kernel, float(smoothing))
+        return _rbf.rbf_field(points, values, grid_tuple, int(rbf_neighbors), rbf_kernel, smoothing,
+                              n_jobs=int(n_jobs))
     # scattered-data griddata methods: not part of the accelerated path (interpolator.py:196-197)
     from scipy.interpolate import griddata
 

@@ -1,0 +1,200 @@
+"""GPU parity of the local-RBF path (``method='rbf'``, interpolator.py:157-195) through the
+C ABI (``ptv_interp_rbf_local``), against the reference golden vectors and the oracle
+(``oracle.cpu_ref.rbf_local_points``).  Runs only on an MI355X (``-m gpu``).
+
+Bar: normwise max|d|/max|ref| per component.  The per-voxel solve is a
+dense LU with partial pivoting; the GPU factors unblocked (one row per lane) where
+scipy's LAPACK dgetrf is blocked, so the results agree to the conditioning of the
+systems, not bit for bit:
+
+* TOL = 1e-10 for every case whose systems have cond <= 1e8 (all reference-reachable
+  kernels at the fixture sizes: TPS, cubic, quintic, linear; cond 4e2 .. 2e7);
+* TOL_ILL = 1e-8 for the Gaussian eps=0.3 fixtures (cond up to 6e8), where two CPU
+  LAPACK builds (numpy's and scipy's OpenBLAS) already differ by 1.6e-9.
+"""
+import numpy as np
+import pandas as pd
+import pytest
+
+from tests._util import load, names, normwise
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-10
+TOL_ILL = 1e-8
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from ptv_interpolation_amd import _lib
+
+    if _lib.device_count() < 1:
+        pytest.fail("no GPU visible: the gpu tests must run on an MI355X")
+    return _lib.Context.get(0)
+
+
+def _df(points, values):
+    return pd.DataFrame({c: points[:, i] for i, c in enumerate("xyz")} | {c: values[:, i] for i, c in enumerate("uvw")})
+
+
+def _tol(g):
+    return TOL_ILL if str(g["kernel"]) == "gaussian" else TOL
+
+
+@pytest.mark.parametrize("name", [n for n in names(("rbf",)) if "gaussian" not in n])
+def test_golden_dropin(ctx, name, capsys):
+    """interpolate_field(method='rbf') on the reference's own fixtures (reachable kernels)."""
+    from ptv_interpolation_amd import interpolator as ip
+
+    g = load(name)
+    n = len(g["ax"])
+    (X, Y, Z), _ = ip.create_grid(((0, n),) * 3, n)
+    assert np.array_equal(X[0, 0], g["ax"])
+    U, V, W = ip.interpolate_field(_df(g["points"], g["values"]), (X, Y, Z), method="rbf",
+                                   rbf_neighbors=int(g["k"]), rbf_kernel=str(g["kernel"]),
+                                   smoothing=float(g["smoothing"]))
+    out = capsys.readouterr().out
+    assert out.startswith(f"Using RBF Interpolation ({g['kernel']}) with {int(g['k'])} neighbors, "
+                          f"smoothing={float(g['smoothing'])} and n_jobs=1...")
+    assert f"Interpolating {n ** 3} points serially..." in out
+    for a, b in ((U, g["U"]), (V, g["V"]), (W, g["W"])):
+        assert a.shape == b.shape and a.dtype == np.float64
+        assert normwise(a, b) <= _tol(g)
+
+
+@pytest.mark.parametrize("name", [n for n in names(("rbf",)) if "gaussian" in n])
+def test_golden_gaussian_scipy_oracle(ctx, name):
+    """RBFInterpolator(kernel='gaussian', epsilon=0.3, degree=0/-1) — scipy oracle cases."""
+    from ptv_interpolation_amd.rbf import LocalRBFInterpolator
+
+    g = load(name)
+    it = LocalRBFInterpolator(g["points"], g["values"], neighbors=int(g["k"]), kernel="gaussian",
+                              epsilon=float(g["epsilon"]), degree=int(g["degree"]),
+                              smoothing=float(g["smoothing"]))
+    U, V, W = it.evaluate_grid(g["ax"], g["ay"], g["az"])
+    for a, b in ((U, g["U"]), (V, g["V"]), (W, g["W"])):
+        assert normwise(a, b) <= TOL_ILL
+
+
+def _rand_case(seed, n, G, lo=0.0, hi=None):
+    rng = np.random.default_rng(seed)
+    hi = float(G - 1) if hi is None else hi
+    P = rng.uniform(lo - 0.5, hi + 0.5, (n, 3))
+    Q = rng.standard_normal((n, 3))
+    ax = np.linspace(lo, hi, G)
+    return P, Q, ax
+
+
+@pytest.mark.parametrize("kernel,k,degree,eps", [
+    ("thin_plate_spline", 20, None, None),
+    ("thin_plate_spline", 32, None, None),
+    ("cubic", 8, None, None),
+    ("quintic", 30, None, None),
+    ("linear", 50, None, None),
+    ("multiquadric", 24, None, 0.8),
+    ("inverse_multiquadric", 24, None, 0.8),
+    ("inverse_quadratic", 24, 1, 0.8),
+    ("gaussian", 32, -1, 1.0),
+    ("gaussian", 60, 0, 1.5),
+    ("thin_plate_spline", 54, 2, None),
+])
+def test_random_vs_oracle(ctx, kernel, k, degree, eps):
+    """Every scipy kernel, system sizes 12..64 (each padded size class), against the oracle."""
+    from oracle import cpu_ref
+    from ptv_interpolation_amd.rbf import LocalRBFInterpolator
+
+    P, Q, ax = _rand_case(k * 7 + len(kernel), 6000, 16)
+    it = LocalRBFInterpolator(P, Q, neighbors=k, kernel=kernel, epsilon=eps, degree=degree)
+    U, V, W = it.evaluate_grid(ax, ax, ax)
+    ref = cpu_ref.rbf_local_grid(P, Q, ax, ax, ax, k, kernel, eps, degree)
+    for a, b in zip((U, V, W), ref):
+        assert normwise(a, b) <= TOL
+
+
+def test_smoothing_scalar_and_per_point(ctx):
+    from oracle import cpu_ref
+    from ptv_interpolation_amd.rbf import LocalRBFInterpolator
+
+    P, Q, ax = _rand_case(11, 4000, 12)
+    sm = np.random.default_rng(12).uniform(0.0, 3.0, len(P))
+    for s in (5.0, sm):
+        U, V, W = LocalRBFInterpolator(P, Q, neighbors=24, smoothing=s).evaluate_grid(ax, ax, ax)
+        ref = cpu_ref.rbf_local_grid(P, Q, ax, ax, ax, 24, smoothing=s)
+        for a, b in zip((U, V, W), ref):
+            assert normwise(a, b) <= TOL
+
+
+def test_point_list_call_and_extra_components(ctx):
+    """__call__ on an (Q, 3) list; 5 value components go through in groups of three."""
+    from oracle import cpu_ref
+    from ptv_interpolation_amd.rbf import LocalRBFInterpolator
+
+    rng = np.random.default_rng(21)
+    P = rng.uniform(0, 10, (3000, 3))
+    D = rng.standard_normal((3000, 5))
+    X = rng.uniform(-1, 11, (777, 3))
+    out = LocalRBFInterpolator(P, D, neighbors=16, kernel="cubic")(X)
+    assert out.shape == (777, 5)
+    ref = cpu_ref.rbf_local_points(P, D, X, 16, "cubic")
+    for c in range(5):
+        assert normwise(out[:, c], ref[:, c]) <= TOL
+
+
+def test_z_slab_and_chunking_equal_whole(ctx):
+    """Chunked k-NN + solve launches and z-slab calls give the whole-grid result bit for bit."""
+    P, Q, ax = _rand_case(31, 5000, 20)
+    k = 20
+    whole = ctx.interp_rbf(P, Q, axes=(ax, ax, ax), k=k)
+    chunked = ctx.interp_rbf(P, Q, axes=(ax, ax, ax), k=k, chunk_planes=4)
+    slab = ctx.interp_rbf(P, Q, axes=(ax, ax, ax), k=k, z_range=(8, 16))
+    for a, b, c in zip(whole, chunked, slab):
+        assert np.array_equal(a, b)
+        assert np.array_equal(a[8:16], c)
+
+
+def test_mask_and_nan_to_num(ctx):
+    from ptv_interpolation_amd import _lib
+
+    P, Q, ax = _rand_case(41, 4000, 12)
+    mask = np.random.default_rng(42).uniform(size=(12, 12, 12)) < 0.6
+    full = ctx.interp_rbf(P, Q, axes=(ax, ax, ax), k=20)
+    m = ctx.interp_rbf(P, Q, axes=(ax, ax, ax), k=20, fluid_mask=mask, flags=_lib.FLAG_NAN_TO_NUM)
+    for a, b in zip(full, m):
+        assert np.array_equal(a[mask], b[mask])
+        assert (b[~mask] == 0).all()
+
+
+def test_singular_system_raises_linalgerror(ctx):
+    """Coplanar particles leave the TPS linear-polynomial block rank deficient (an exactly
+    zero column): scipy's dgesv reports info > 0 and RBFInterpolator raises LinAlgError."""
+    from ptv_interpolation_amd.rbf import LocalRBFInterpolator
+
+    rng = np.random.default_rng(5)
+    P = rng.uniform(0, 4, (40, 3))
+    P[:, 2] = 1.0
+    Q = rng.standard_normal((40, 3))
+    ax = np.linspace(0, 3, 4)
+    with pytest.raises(np.linalg.LinAlgError, match="Singular matrix"):
+        LocalRBFInterpolator(P, Q, neighbors=20).evaluate_grid(ax, ax, ax)
+
+
+def test_full_size_sampled(ctx):
+    """C3 shape at a reduced grid: 128^3 over a 5M-particle-density sphere pack slice, TPS k=32,
+    checked on 3000 random voxels against the oracle."""
+    from oracle import cpu_ref
+    from ptv_interpolation_amd.rbf import LocalRBFInterpolator
+
+    rng = np.random.default_rng(77)
+    G = 128
+    n = 5_000_000 * G ** 3 // 512 ** 3
+    P = rng.uniform(-0.5, G - 0.5, (n, 3))
+    Q = rng.standard_normal((n, 3))
+    ax = np.arange(G, dtype=np.float64)
+    it = LocalRBFInterpolator(P, Q, neighbors=32, kernel="thin_plate_spline")
+    U, V, W = it.evaluate_grid(ax, ax, ax)
+    sel = rng.integers(0, G ** 3, 3000)
+    iz, iy, ix = np.unravel_index(sel, (G, G, G))
+    q = np.stack([ax[ix], ax[iy], ax[iz]], -1)
+    ref = cpu_ref.rbf_local_points(P, Q, q, 32, "thin_plate_spline")
+    for c, a in enumerate((U, V, W)):
+        assert normwise(a.ravel()[sel], ref[:, c]) <= TOL

@@ -99,3 +99,33 @@ def test_sphere_pack_is_seeded_and_exact_count():
     lo, hi = synth.LO, synth.HI
     D = lo + P1 / 39.0 * (hi - lo)
     assert not synth.inside_spheres(D[:, 0], D[:, 1], D[:, 2]).any()
+
+
+def test_rbf_argument_resolution_matches_scipy():
+    """LocalRBFInterpolator raises what scipy's RBFInterpolator raises (_rbfinterp.py:258-345),
+    before any GPU call."""
+    import warnings
+
+    from scipy.interpolate import RBFInterpolator
+
+    from ptv_interpolation_amd.rbf import LocalRBFInterpolator
+
+    rng = np.random.default_rng(0)
+    P, D = rng.uniform(0, 5, (30, 3)), rng.standard_normal((30, 3))
+    bad = [dict(kernel="nope"), dict(kernel="gaussian"), dict(degree=-2), dict(neighbors=3, degree=1),
+           dict(smoothing=np.ones(7))]
+    for kw in bad:
+        kw.setdefault("neighbors", 10)
+        with pytest.raises(Exception) as ref:
+            RBFInterpolator(P, D, **kw)
+        with pytest.raises(type(ref.value)) as mine:
+            LocalRBFInterpolator(P, D, **kw)
+        assert str(mine.value)[:24] == str(ref.value)[:24]
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        LocalRBFInterpolator(P, D, neighbors=10, kernel="thin_plate_spline", degree=0)
+    assert any(issubclass(x.category, UserWarning) for x in w)
+    it = LocalRBFInterpolator(P, D, neighbors=50)  # k clamps to n (_rbfinterp.py:322)
+    assert it.neighbors == 30 and it.degree == 1 and it.epsilon == 1.0
+    with pytest.raises(NotImplementedError):
+        LocalRBFInterpolator(np.tile(P, (3, 1)), np.tile(D, (3, 1)), neighbors=61)  # 61 + 4 > 64

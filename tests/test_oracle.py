@@ -61,3 +61,41 @@ def test_parallel_driver_equals_whole_grid():
     U0, V0, W0 = cpu_ref.interp_grid(g["points"], g["values"], g["ax"], g["ay"], g["az"], "idw", 8, 2.0)
     U1, V1, W1 = cpu_ref.interp_grid_parallel(g["points"], g["values"], g["ax"], g["ay"], g["az"], "idw", 8, 2.0, n_jobs=2)
     assert np.array_equal(U0, U1) and np.array_equal(V0, V1) and np.array_equal(W0, W1)
+
+
+def _rbf_args(g):
+    eps = float(g["epsilon"]) if "epsilon" in g else None
+    deg = int(g["degree"]) if "degree" in g else None
+    return int(g["k"]), str(g["kernel"]), eps, deg, float(g["smoothing"])
+
+
+@pytest.mark.parametrize("name", names(("rbf",)))
+def test_rbf_oracle_matches_reference(name):
+    """The local-RBF restatement (scipy RBFInterpolator(neighbors=k) via numpy's LAPACK gesv)
+    against the reference's own outputs.  The Gaussian eps=0.3 systems reach cond 6e8: two
+    LAPACK builds differ there by 1.6e-9, so those fixtures get 1e-8 (tests/test_gpu_rbf.py)."""
+    g = load(name)
+    k, kern, eps, deg, s = _rbf_args(g)
+    U, V, W = cpu_ref.rbf_local_grid(g["points"], g["values"], g["ax"], g["ay"], g["az"], k, kern, eps, deg, s)
+    tol = 1e-8 if kern == "gaussian" else 1e-11
+    for a, b in ((U, g["U"]), (V, g["V"]), (W, g["W"])):
+        assert normwise(a, b) <= tol
+
+
+def test_rbf_monomial_powers_match_scipy():
+    from scipy.interpolate._rbfinterp import _monomial_powers
+
+    for deg in range(-1, 4):
+        assert np.array_equal(cpu_ref.monomial_powers(deg), _monomial_powers(3, deg))
+
+
+@pytest.mark.parametrize("kernel", sorted(cpu_ref.RBF_PHI))
+def test_rbf_kernel_formulas_match_scipy(kernel):
+    """phi(r) against scipy's compiled kernel matrix builder on one small point set."""
+    from scipy.interpolate._rbfinterp_pythran import _kernel_matrix
+
+    rng = np.random.default_rng(1)
+    y = rng.uniform(0, 3, (20, 3))
+    ref = _kernel_matrix(y, kernel)
+    r = np.sqrt(((y[:, None, :] - y[None, :, :]) ** 2).sum(-1))
+    assert np.allclose(cpu_ref.RBF_PHI[kernel](r), ref, rtol=1e-13, atol=1e-14)
