@@ -42,7 +42,27 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "Mvoxels/s interpolated + achieved HBM GB/s, 512³ grid / 5M particles IDW"
+METRIC_RBF = "Mvoxels/s interpolated + achieved FP64 TFLOP/s, 512³ grid / 5M particles local RBF"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec (AMD); not listed in the guide
+
+
+def rbf_resolved(args):
+    """(kernel, epsilon, degree, m) with scipy's defaults (_rbfinterp.py:300-313)."""
+    from math import comb
+
+    from ptv_interpolation_amd import rbf
+
+    kern = args.rbf_kernel
+    eps = args.epsilon if args.epsilon is not None else 1.0
+    deg = args.degree if args.degree is not None else max(rbf.NAME_TO_MIN_DEGREE.get(kern, -1), 0)
+    m = args.k + (comb(deg + 3, 3) if deg >= 0 else 0)
+    return kern, eps, deg, m
+
+
+def rbf_flops_per_voxel(k, m):
+    """distances 8 k(k-1)/2, LU (2/3) m^3, substitution + build 6 m^2, eval 8k + 6m."""
+    return 8 * k * (k - 1) / 2 + (2.0 / 3.0) * m ** 3 + 6 * m ** 2 + 8 * k + 6 * m
 
 
 def parse():
@@ -54,7 +74,10 @@ def parse():
     ap.add_argument("--particles", type=int, default=5_000_000)
     ap.add_argument("--k", type=int, default=8)
     ap.add_argument("--power", type=float, default=2.0)
-    ap.add_argument("--method", default="idw", choices=["idw", "sibson"])
+    ap.add_argument("--method", default="idw", choices=["idw", "sibson", "rbf"])
+    ap.add_argument("--rbf-kernel", default="thin_plate_spline", help="--method rbf: scipy kernel name")
+    ap.add_argument("--epsilon", type=float, default=None, help="--method rbf: shape parameter")
+    ap.add_argument("--degree", type=int, default=None, help="--method rbf: polynomial degree")
     ap.add_argument("--halo", type=int, default=64, help="neighbour-copy halo (voxels) for N>1")
     ap.add_argument("--cpu-sample-planes", type=int, default=16)
     ap.add_argument("--cpu-workers", type=int, default=16)
@@ -114,6 +137,37 @@ def cpu_baseline(args, P, Q, ax):
             "seconds": round(dt, 2)}
 
 
+def _rbf_cpu_worker(a):
+    from oracle import cpu_ref
+
+    P, Q, q, k, kern, eps, deg = a
+    return cpu_ref.rbf_local_points(P, Q, q, k, kern, eps, deg)
+
+
+def cpu_baseline_rbf(args, P, Q, ax):
+    """Oracle local RBF (KDTree + per-voxel LAPACK gesv) on a bounded voxel sample, split over a
+    ProcessPoolExecutor like interpolator.py:173-182 (each worker builds its own tree)."""
+    from concurrent.futures import ProcessPoolExecutor
+
+    kern, eps, deg, _ = rbf_resolved(args)
+    workers = max(1, min(args.cpu_workers, os.cpu_count() or 1))
+    nvox = 2048 * workers
+    G = len(ax)
+    rng = np.random.default_rng(0)
+    sel = rng.integers(0, G ** 3, nvox)
+    iz, iy, ix = np.unravel_index(sel, (G, G, G))
+    q = np.stack([ax[ix], ax[iy], ax[iz]], -1)
+    t = time.perf_counter()
+    with ProcessPoolExecutor(max_workers=workers) as ex:
+        list(ex.map(_rbf_cpu_worker, [(P, Q, c, args.k, kern, eps, deg) for c in np.array_split(q, workers)]))
+    dt = time.perf_counter() - t
+    return {"value": round(nvox / dt / 1e6, 6), "unit": "Mvoxels/s", "cores": workers, "kind": "port",
+            "sample": f"{nvox} random voxels of the same {G}^3/{args.particles} workload; scipy KDTree + numpy "
+                      f"LAPACK gesv per voxel (oracle/cpu_ref.rbf_local_points), {workers} processes, each "
+                      f"building its own tree (interpolator.py:173-182 pattern)",
+            "seconds": round(dt, 2)}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -148,11 +202,20 @@ def main():
     method = _lib.METHOD_IDW if args.method == "idw" else _lib.METHOD_SIBSON
     stream = torch.cuda.current_stream(dev).cuda_stream
 
-    def step():
-        return ctx.interp_knn_dev(n, [c.data_ptr() for c in cols], G, G, G,
-                                  axes_ptrs=[a.data_ptr() for a in axes],
-                                  out_ptrs=[o.data_ptr() for o in out], method=method, k=args.k,
-                                  power=args.power, stream=stream)
+    if args.method == "rbf":
+        kern, eps, deg, m_sys = rbf_resolved(args)
+
+        def step():
+            return ctx.interp_rbf_dev(n, [c.data_ptr() for c in cols], G, G, G,
+                                      axes_ptrs=[a.data_ptr() for a in axes],
+                                      out_ptrs=[o.data_ptr() for o in out], k=args.k, kernel=kern, epsilon=eps,
+                                      degree=deg, stream=stream)
+    else:
+        def step():
+            return ctx.interp_knn_dev(n, [c.data_ptr() for c in cols], G, G, G,
+                                      axes_ptrs=[a.data_ptr() for a in axes],
+                                      out_ptrs=[o.data_ptr() for o in out], method=method, k=args.k,
+                                      power=args.power, stream=stream)
 
     for _ in range(args.warmup):
         step()
@@ -160,7 +223,7 @@ def main():
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    knn_ms, lat_ms, bin_ms = [], [], []
+    knn_ms, lat_ms, bin_ms, solve_ms = [], [], [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -168,6 +231,7 @@ def main():
         knn_ms.append(st["ms_knn"])
         lat_ms.append(st["ms_lattice"])
         bin_ms.append(st["ms_bin"])
+        solve_ms.append(st["ms_solve"])
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
@@ -198,16 +262,29 @@ def main():
     achieved = alg_bytes / (knn_avg * 1e-3) / 1e9
     traffic = traffic_from_profiles()
 
+    if args.method == "rbf":
+        solve_avg = float(np.mean(solve_ms))
+        flops = vox * rbf_flops_per_voxel(args.k, m_sys)
+        tf = flops / (solve_avg * 1e-3) / 1e12
+        roof = {"bound": "fp64", "achieved": round(tf, 2), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(tf / FP64_PEAK_TFLOPS, 4), "traffic": None, "kernel": "k_rbf_local",
+                "alg_flops_per_launch": flops, "kernel_ms": round(solve_avg, 3)}
+    else:
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic": traffic, "kernel": f"k_knn_interp<{args.k}>",
+                "alg_bytes_per_launch": alg_bytes, "kernel_ms": round(knn_avg, 3)}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            cpu = cpu_baseline(args, P, Q, ax_h)
+            cpu = (cpu_baseline_rbf if args.method == "rbf" else cpu_baseline)(args, P, Q, ax_h)
         except Exception as e:  # the baseline must never take the GPU line down
             cpu = {"value": None, "error": repr(e)[:200]}
 
     if rank == 0:
         line = {
-            "metric": METRIC,
+            "metric": METRIC_RBF if args.method == "rbf" else METRIC,
             "value": round(value, 2),
             "unit": "Mvoxels/s",
             "n_gpus": world,
@@ -219,18 +296,18 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic: generate_sphere_pack.py geometry scaled to voxel units, seeded, w=1 flow field",
-            "config": {"workload": f"{G}^3 grid / {args.particles} particles {args.method.upper()} "
-                                   f"k={args.k} p={args.power} fp64 (z-slab per GPU)",
+            "config": {"workload": (f"{G}^3 grid / {args.particles} particles local RBF {kern} k={args.k} "
+                                    f"eps={eps} degree={deg} (system {m_sys}) fp64 (z-slab per GPU)")
+                       if args.method == "rbf" else
+                       f"{G}^3 grid / {args.particles} particles {args.method.upper()} "
+                       f"k={args.k} p={args.power} fp64 (z-slab per GPU)",
                        "grid": G, "particles": args.particles, "particles_binned_rank0": n,
                        "method": args.method, "k": args.k, "power": args.power,
                        "parallelism": f"z-slab x{world}"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic, "kernel": "k_knn_interp<8>",
-                         "alg_bytes_per_launch": alg_bytes, "kernel_ms": round(knn_avg, 3)},
+            "roofline": roof,
             "cpu_baseline": cpu,
             "breakdown_ms": {"bin": round(float(np.mean(bin_ms)), 3), "lattice": round(float(np.mean(lat_ms)), 3),
-                             "knn": round(knn_avg, 3)},
+                             "knn": round(knn_avg, 3), "solve": round(float(np.mean(solve_ms)), 3)},
         }
         if gather_ms is not None:
             line["allgather_ms"] = round(gather_ms, 2)
