@@ -77,13 +77,16 @@ __device__ double rbf_phi_rt(int kern, double r) {
     }
 }
 
+// libm pow for the rare exponents > 3 (degree >= 4); out of line so its code exists once
+__device__ __noinline__ double ipow_slow(double x, int p) { return pow(x, (double)p); }
+
 // x ** p for the small integer monomial exponents (np.prod(x ** powers[j]))
 __device__ __forceinline__ double ipow(double x, int p) {
     if (p == 0) return 1.0;
     if (p == 1) return x;
     if (p == 2) return x * x;
     if (p == 3) return (x * x) * x;
-    return pow(x, (double)p);
+    return ipow_slow(x, p);
 }
 
 // monomial with exponents packed as px | py << 8 | pz << 16
@@ -91,47 +94,127 @@ __device__ __forceinline__ double mono(double hx, double hy, double hz, int code
     return (ipow(hx, code & 255) * ipow(hy, (code >> 8) & 255)) * ipow(hz, code >> 16);
 }
 
+// ---- segment reductions in registers: DPP within 16-lane rows (quad_perm xor 1, xor 2,
+// row_half_mirror, row_mirror), v_permlane16_swap / v_permlane32_swap (gfx950) across rows.
+// Every lane of the segment ends with the same value (each step combines symmetric pairs). ----
+template <int CTRL>
+__device__ __forceinline__ unsigned dpp_u32(unsigned v) {
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = dpp_u32<CTRL>((unsigned)b), hi = dpp_u32<CTRL>((unsigned)(b >> 32));
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+// (v of this lane's row partner, v of its half-wave partner): the two results of a swap of v with itself
+template <int W>
+__device__ __forceinline__ void swap_self(unsigned v, unsigned &a, unsigned &b) {
+    if constexpr (W == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        a = r[0];
+        b = r[1];
+    } else {
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        a = r[0];
+        b = r[1];
+    }
+}
+template <int W>
+__device__ __forceinline__ void swap_self_f64(double v, double &a, double &b) {
+    const unsigned long long x = (unsigned long long)__double_as_longlong(v);
+    unsigned al, bl, ah, bh;
+    swap_self<W>((unsigned)x, al, bl);
+    swap_self<W>((unsigned)(x >> 32), ah, bh);
+    a = __longlong_as_double((long long)(((unsigned long long)ah << 32) | al));
+    b = __longlong_as_double((long long)(((unsigned long long)bh << 32) | bl));
+}
+
+template <int L, typename Op>
+__device__ __forceinline__ double seg_reduce(double v, Op op) {
+    static_assert(L == 16 || L == 32 || L == 64, "segment width");
+    v = op(v, dpp_f64<0xB1>(v));   // quad_perm [1,0,3,2]
+    v = op(v, dpp_f64<0x4E>(v));   // quad_perm [2,3,0,1]
+    v = op(v, dpp_f64<0x141>(v));  // row_half_mirror
+    v = op(v, dpp_f64<0x140>(v));  // row_mirror
+    if constexpr (L >= 32) {
+        double a, b;
+        swap_self_f64<16>(v, a, b);
+        v = op(a, b);
+    }
+    if constexpr (L == 64) {
+        double a, b;
+        swap_self_f64<32>(v, a, b);
+        v = op(a, b);
+    }
+    return v;
+}
+template <int L>
+__device__ __forceinline__ unsigned seg_max_u32(unsigned v) {
+    v = max(v, dpp_u32<0xB1>(v));
+    v = max(v, dpp_u32<0x4E>(v));
+    v = max(v, dpp_u32<0x141>(v));
+    v = max(v, dpp_u32<0x140>(v));
+    if constexpr (L >= 32) {
+        unsigned a, b;
+        swap_self<16>(v, a, b);
+        v = max(a, b);
+    }
+    if constexpr (L == 64) {
+        unsigned a, b;
+        swap_self<32>(v, a, b);
+        v = max(a, b);
+    }
+    return v;
+}
 template <int L>
 __device__ __forceinline__ double seg_sum(double v) {
-#pragma unroll
-    for (int o = 1; o < L; o <<= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    return seg_reduce<L>(v, [](double x, double y) { return x + y; });
 }
 template <int L>
 __device__ __forceinline__ double seg_min(double v) {
-#pragma unroll
-    for (int o = 1; o < L; o <<= 1) v = fmin(v, __shfl_xor(v, o, 64));
-    return v;
+    return seg_reduce<L>(v, [](double x, double y) { return fmin(x, y); });
 }
 template <int L>
 __device__ __forceinline__ double seg_max(double v) {
-#pragma unroll
-    for (int o = 1; o < L; o <<= 1) v = fmax(v, __shfl_xor(v, o, 64));
-    return v;
-}
-template <int L>
-__device__ __forceinline__ int seg_min_i(int v) {
-#pragma unroll
-    for (int o = 1; o < L; o <<= 1) v = min(v, __shfl_xor(v, o, 64));
-    return v;
+    return seg_reduce<L>(v, [](double x, double y) { return fmax(x, y); });
 }
 
-// kernel block of row i: A[j] = phi(eps*|y_i - y_j|) (+ s_i on the diagonal) for j < k
-template <int M, int KERN>
-__device__ __forceinline__ void build_kernel_block(double (&A)[M], const double4 *__restrict__ ye, double4 yi,
-                                                   int k, int li, bool krow, double si) {
-#pragma unroll
-    for (int j = 0; j < M; ++j) {
-        if (j < k) {
-            const double4 yj = ye[j];
-            const double dx = yi.x - yj.x, dy = yi.y - yj.y, dz = yi.z - yj.z;
-            const double r = sqrt((dx * dx + dy * dy) + dz * dz);
-            double p = rbf_phi<KERN>(r);
-            if (j == li) p = p + si;
-            if (krow) A[j] = p;
+// Entries j in [j0, j0 + n) of system row li, into the lane's column of the per-wave LDS
+// scratch (sc[jj * 64 + lane]).  A rolled loop: the phi / monomial code is emitted once, so
+// the kernel stays small (a fully unrolled build is M copies of log/exp/sqrt and thrashes
+// the instruction cache).
+template <int KERN>
+__device__ __forceinline__ void build_entries(double *__restrict__ sc, int lane, int j0, int n, int k, int m, int li,
+                                              const double4 *__restrict__ ye, const double4 *__restrict__ yh,
+                                              double4 yi, double4 hi, double si, const int *__restrict__ pw,
+                                              int tcode) {
+#pragma unroll 1
+    for (int jj = 0; jj < n; ++jj) {
+        const int j = j0 + jj;
+        double e = 0.0;
+        if (li < k) {
+            if (j < k) {
+                const double4 yj = ye[j];
+                const double dx = yi.x - yj.x, dy = yi.y - yj.y, dz = yi.z - yj.z;
+                e = rbf_phi<KERN>(sqrt((dx * dx + dy * dy) + dz * dz));
+                if (j == li) e = e + si;
+            } else if (j < m) {
+                e = mono(hi.x, hi.y, hi.z, pw[j - k]);
+            }
+        } else if (li < m) {
+            if (j < k) {
+                const double4 hj = yh[j];
+                e = mono(hj.x, hj.y, hj.z, tcode);
+            }
+        } else {
+            e = j == li ? 1.0 : 0.0;  // identity padding up to M
         }
+        sc[jj * 64 + lane] = e;
     }
 }
+
+constexpr int kBuildCols = 16;  // system columns built per LDS round
 
 template <int M, int L>
 __global__ __launch_bounds__(256) void k_rbf_local(RbfKernelArgs a, const double4 *__restrict__ prec,
@@ -151,6 +234,7 @@ __global__ __launch_bounds__(256) void k_rbf_local(RbfKernelArgs a, const double
     __shared__ double4 s_val[4][64];  // data values (u, v, w) in id order; later the solution
     __shared__ double s_row[4][SPW][M + 4];
     __shared__ uint32_t s_id[4][64];
+    __shared__ double s_build[4][kBuildCols * 64];  // row build scratch, [column][lane]
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int seg = lane / L, li = lane % L, sb = seg * L;
     double4 *ye = s_ye[wid] + sb;
@@ -211,47 +295,37 @@ __global__ __launch_bounds__(256) void k_rbf_local(RbfKernelArgs a, const double
     }
     rbf_wave_sync();
 
-    // ---- 2. row li of the system ----
+    // ---- 2. row li of the system: [phi + s_i delta | P(yhat_i)] for kernel rows, [P(yhat_j)^T | 0]
+    // for the polynomial rows, identity padding up to M; built BH columns at a time through LDS ----
     const bool krow = li < k;
-    const bool prow = li >= k && li < m;
     double A[M];
-#pragma unroll
-    for (int j = 0; j < M; ++j) A[j] = 0.0;
     const double4 yi = krow ? ye[li] : make_double4(0.0, 0.0, 0.0, 0.0);
+    const double4 hi = krow ? yh[li] : make_double4(0.0, 0.0, 0.0, 0.0);
+    const int tcode = (li >= k && li < m) ? pw[li - k] : 0;
     double si = 0.0;
     if (krow && active) si = smooth != nullptr ? smooth[(size_t)yi.w] : a.smoothing;
-    switch (a.kernel) {
-        case PTV_RBF_LINEAR: build_kernel_block<M, PTV_RBF_LINEAR>(A, ye, yi, k, li, krow, si); break;
-        case PTV_RBF_THIN_PLATE_SPLINE: build_kernel_block<M, PTV_RBF_THIN_PLATE_SPLINE>(A, ye, yi, k, li, krow, si); break;
-        case PTV_RBF_CUBIC: build_kernel_block<M, PTV_RBF_CUBIC>(A, ye, yi, k, li, krow, si); break;
-        case PTV_RBF_QUINTIC: build_kernel_block<M, PTV_RBF_QUINTIC>(A, ye, yi, k, li, krow, si); break;
-        case PTV_RBF_MULTIQUADRIC: build_kernel_block<M, PTV_RBF_MULTIQUADRIC>(A, ye, yi, k, li, krow, si); break;
-        case PTV_RBF_INVERSE_MULTIQUADRIC:
-            build_kernel_block<M, PTV_RBF_INVERSE_MULTIQUADRIC>(A, ye, yi, k, li, krow, si);
-            break;
-        case PTV_RBF_INVERSE_QUADRATIC: build_kernel_block<M, PTV_RBF_INVERSE_QUADRATIC>(A, ye, yi, k, li, krow, si); break;
-        default: build_kernel_block<M, PTV_RBF_GAUSSIAN>(A, ye, yi, k, li, krow, si); break;
-    }
-    if (m > k) {
-        // polynomial blocks: P(yhat_i) in the columns k..m-1 of the kernel rows, P(yhat_j)^T in
-        // the rows k..m-1, zeros in the bottom-right corner
-        const double4 hi = krow ? yh[li] : make_double4(0.0, 0.0, 0.0, 0.0);
-        const int tcode = prow ? pw[li - k] : 0;
+    double *sc = s_build[wid];
 #pragma unroll
-        for (int j = 0; j < M; ++j) {
-            if (j < k) {
-                const double4 hj = yh[j];
-                const double p = mono(hj.x, hj.y, hj.z, tcode);
-                if (prow) A[j] = p;
-            } else if (j < m) {
-                const double p = mono(hi.x, hi.y, hi.z, pw[j - k]);
-                if (krow) A[j] = p;
-            }
+    for (int g = 0; g < M; g += kBuildCols) {
+        const int n = M - g < kBuildCols ? M - g : kBuildCols;
+        switch (a.kernel) {
+#define PTV_BCASE(KK) \
+    case KK: build_entries<KK>(sc, lane, g, n, k, m, li, ye, yh, yi, hi, si, pw, tcode); break;
+            PTV_BCASE(PTV_RBF_LINEAR)
+            PTV_BCASE(PTV_RBF_THIN_PLATE_SPLINE)
+            PTV_BCASE(PTV_RBF_CUBIC)
+            PTV_BCASE(PTV_RBF_QUINTIC)
+            PTV_BCASE(PTV_RBF_MULTIQUADRIC)
+            PTV_BCASE(PTV_RBF_INVERSE_MULTIQUADRIC)
+            PTV_BCASE(PTV_RBF_INVERSE_QUADRATIC)
+            default: build_entries<PTV_RBF_GAUSSIAN>(sc, lane, g, n, k, m, li, ye, yh, yi, hi, si, pw, tcode);
+#undef PTV_BCASE
         }
-    }
+        // each lane reads back only its own column of the scratch: no cross-lane hazard
 #pragma unroll
-    for (int j = 0; j < M; ++j)
-        if (j >= m && li == j) A[j] = 1.0;  // identity padding up to M
+        for (int jj = 0; jj < kBuildCols; ++jj)
+            if (g + jj < M) A[g + jj] = sc[jj * 64 + lane];
+    }
     double b0 = 0.0, b1 = 0.0, b2 = 0.0;
     if (krow) {
         const double4 dv = sv[li];
@@ -261,26 +335,25 @@ __global__ __launch_bounds__(256) void k_rbf_local(RbfKernelArgs a, const double
     }
 
     // ---- 3. Gaussian elimination with partial pivoting; rows stay in their lanes ----
+    // Pivot choice as one u32 segment max: the key is the top bits of |A[c]| (exponent and 13
+    // mantissa bits; a nonzero value never maps to class 0) above (64 - pos), so the largest
+    // |a| wins and, among keys equal in those bits, the lowest LAPACK row position (idamax's
+    // first index).  The pivot row goes to the segment through LDS; every other row updates
+    // branch-free (l = 0 for finished rows).
     bool done = li >= M;  // lanes beyond the padded system never pivot
-    int pos = li;         // LAPACK row position (idamax tie order)
+    int pos = li;         // LAPACK row position
     int mystep = -1;      // the elimination step that used this row as pivot
+    double diag = 1.0;    // this row's pivot (U diagonal entry)
     bool singular = false;
 #pragma unroll
     for (int c = 0; c < M; ++c) {
-        const double key = done ? -1.0 : fabs(A[c]);
-        const double mx = seg_max<L>(key);
-        const bool cand = !done && key == mx;
-        unsigned long long bal = __builtin_amdgcn_ballot_w64(cand);
-        unsigned long long sbal = L == 64 ? bal : ((bal >> sb) & ((1ull << (L & 63)) - 1ull));
-        if (__builtin_amdgcn_ballot_w64(__builtin_popcountll(sbal) > 1) != 0) {
-            // ties: the lowest current row position wins (first index of idamax)
-            const int pk = seg_min_i<L>(cand ? pos : 0x7fffffff);
-            bal = __builtin_amdgcn_ballot_w64(cand && pos == pk);
-            sbal = L == 64 ? bal : ((bal >> sb) & ((1ull << (L & 63)) - 1ull));
-        }
-        const int P = (int)__builtin_ctzll(sbal | (1ull << 63));
-        const bool isP = li == P;
-        singular = singular || !(mx > 0.0);
+        const unsigned long long ab = (unsigned long long)__double_as_longlong(fabs(A[c]));
+        unsigned hi = (unsigned)(ab >> 32);
+        hi = (ab != 0ull && hi < 128u) ? 128u : hi;
+        const unsigned key = done ? 0u : ((hi & ~127u) | (unsigned)(64 - pos));
+        const unsigned mk = seg_max_u32<L>(key);
+        const bool isP = key == mk;
+        singular = singular || (mk >> 7) == 0u;
         if (isP) {
 #pragma unroll
             for (int j = c; j < M; ++j) prow_buf[j] = A[j];
@@ -288,37 +361,34 @@ __global__ __launch_bounds__(256) void k_rbf_local(RbfKernelArgs a, const double
             prow_buf[M + 1] = b1;
             prow_buf[M + 2] = b2;
             prow_buf[M + 3] = (double)pos;
+            diag = A[c];
+            mystep = c;
         }
         rbf_wave_sync();
         const double piv = prow_buf[c];
-        if (isP) {
-            done = true;
-            mystep = c;
-        } else if (!done) {
-            if (pos == c) pos = (int)prow_buf[M + 3];  // the swap moves this row to the pivot's position
-            if (piv != 0.0) {
-                const double l = A[c] * (1.0 / piv);
+        const bool upd = !done && !isP;
+        if (upd && pos == c) pos = (int)prow_buf[M + 3];  // the swap moves this row to the pivot's position
+        const double l = (upd && piv != 0.0) ? A[c] * (1.0 / piv) : 0.0;
 #pragma unroll
-                for (int j = c + 1; j < M; ++j) A[j] = fma(-l, prow_buf[j], A[j]);
-                b0 = fma(-l, prow_buf[M], b0);
-                b1 = fma(-l, prow_buf[M + 1], b1);
-                b2 = fma(-l, prow_buf[M + 2], b2);
-            }
-        }
+        for (int j = c + 1; j < M; ++j) A[j] = fma(-l, prow_buf[j], A[j]);
+        b0 = fma(-l, prow_buf[M], b0);
+        b1 = fma(-l, prow_buf[M + 1], b1);
+        b2 = fma(-l, prow_buf[M + 2], b2);
+        done = done || isP;
         rbf_wave_sync();
     }
 
     // ---- 4. back substitution (column oriented, dtrsm order); solution in LDS ----
+    const double rdiag = 1.0 / diag;
 #pragma unroll
     for (int c = M - 1; c >= 0; --c) {
-        if (mystep == c) sv[c] = make_double4(b0 / A[c], b1 / A[c], b2 / A[c], 0.0);
+        if (mystep == c) sv[c] = make_double4(b0 * rdiag, b1 * rdiag, b2 * rdiag, 0.0);
         rbf_wave_sync();
-        if (mystep >= 0 && mystep < c) {
-            const double4 xc = sv[c];
-            b0 = fma(-A[c], xc.x, b0);
-            b1 = fma(-A[c], xc.y, b1);
-            b2 = fma(-A[c], xc.z, b2);
-        }
+        const double4 xc = sv[c];
+        const double u = (mystep >= 0 && mystep < c) ? A[c] : 0.0;
+        b0 = fma(-u, xc.x, b0);
+        b1 = fma(-u, xc.y, b1);
+        b2 = fma(-u, xc.z, b2);
     }
 
     // ---- 5. evaluate at the voxel: [phi(eps*|x - y_j|), P(xhat)] . coeffs ----
