@@ -5,6 +5,8 @@
 // grow-only device buffers reused across calls (the reference rebuilds its KDTree on
 // every call, interpolator.py:90/:132; here the binning runs every call too, but no
 // allocation does once the buffers are warm).
+#include <cstdio>
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -822,6 +824,12 @@ int ptv_debug_stamps(ptv_ctx *c, int mode, double *out) {
         PTV_HIP(hipDeviceSynchronize());
         std::vector<unsigned long long> h((size_t)cap * nf);
         PTV_HIP(hipMemcpy(h.data(), c->dbg.p, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        if (const char *dump = std::getenv("PTV_STAMPS_DUMP")) {  // raw per-wave records (dev tool)
+            if (FILE *f = std::fopen(dump, "wb")) {
+                std::fwrite(h.data(), sizeof(unsigned long long), h.size(), f);
+                std::fclose(f);
+            }
+        }
         // out: [records, mean of 11 fields, max of 11 fields]: 6 phase cycle counts, then
         // gathered candidates, merge iterations, rounds, passes, candidates kept by the
         // sub-ball filter (packed two or three to a u64 in fields 6 and 7)

@@ -38,6 +38,7 @@
 
 #include "../../include/ptv_api.h"
 #include "ptv_kernels.hpp"
+#include "ptv_wave.hpp"
 
 namespace ptv {
 
@@ -128,39 +129,11 @@ __device__ __forceinline__ double uniform(double v) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-__device__ __forceinline__ double wave_min(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
-    return v;
-}
-__device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-    return v;
-}
-__device__ __forceinline__ int wave_max_i(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
-    return v;
-}
-__device__ __forceinline__ int wave_incl_max_scan_i(int v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        int t = __shfl_up(v, o, 64);
-        if (lane >= o) v = max(v, t);
-    }
-    return v;
-}
-__device__ __forceinline__ int wave_incl_scan_i(int v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        int t = __shfl_up(v, o, 64);
-        if (lane >= o) v += t;
-    }
-    return v;
-}
+__device__ __forceinline__ double wave_min(double v) { return group_reduce<0x3f>(v, OpMin{}); }
+__device__ __forceinline__ double wave_max(double v) { return group_reduce<0x3f>(v, OpMax{}); }
+__device__ __forceinline__ int wave_max_i(int v) { return group_reduce<0x3f>(v, OpMax{}); }
+__device__ __forceinline__ int wave_incl_max_scan_i(int v) { return wave_incl_scan_max(v); }
+__device__ __forceinline__ int wave_incl_scan_i(int v) { return wave_incl_scan_add(v); }
 
 // order this wave's LDS writes before its later reads (and vice versa)
 __device__ __forceinline__ void wave_lds_sync() {
@@ -454,22 +427,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
         float sb_hd;                              // this lane's sub-box half-diagonal (rounded up)
         {
             // extent of this lane's x-half (lanes agreeing in bit 1), y-half (bit 3), z-half (bit 5)
-            float mnx = qfx, mxx = qfx, mny = qfy, mxy = qfy, mnz = qfz, mxz = qfz;
-#pragma unroll
-            for (int o = 1; o <= 32; o <<= 1) {
-                if (o != 2) {
-                    mnx = fminf(mnx, __shfl_xor(mnx, o, 64));
-                    mxx = fmaxf(mxx, __shfl_xor(mxx, o, 64));
-                }
-                if (o != 8) {
-                    mny = fminf(mny, __shfl_xor(mny, o, 64));
-                    mxy = fmaxf(mxy, __shfl_xor(mxy, o, 64));
-                }
-                if (o != 32) {
-                    mnz = fminf(mnz, __shfl_xor(mnz, o, 64));
-                    mxz = fmaxf(mxz, __shfl_xor(mxz, o, 64));
-                }
-            }
+            const float mnx = group_reduce<0x3d>(qfx, OpMin{}), mxx = group_reduce<0x3d>(qfx, OpMax{});
+            const float mny = group_reduce<0x37>(qfy, OpMin{}), mxy = group_reduce<0x37>(qfy, OpMax{});
+            const float mnz = group_reduce<0x1f>(qfz, OpMin{}), mxz = group_reduce<0x1f>(qfz, OpMax{});
             const float ux = mxx - mnx, uy = mxy - mny, uz = mxz - mnz;
             sb_hd = 0.5f * sqrtf_up(__fmaf_rn(uz, uz, __fmaf_rn(uy, uy, ux * ux)) * 1.000001f) * 1.00001f;
             const float cxs = 0.5f * (mnx + mxx), cys = 0.5f * (mny + mxy), czs = 0.5f * (mnz + mxz);
@@ -484,8 +444,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
         auto subballs = [&]() {
             // radius of sub-ball s: max over its 8 lanes of sqrt(thr) + the half-diagonal
             float rv = thr < 0.0 ? -1.0f : sqrtf_up((float)(thr * (1.0 + 2.384185791015625e-07)));
-#pragma unroll
-            for (int o = 1; o <= 16; o <<= 2) rv = fmaxf(rv, __shfl_xor(rv, o, 64));
+            rv = group_reduce<0x15>(rv, OpMax{});
             const float Rs = (rv + sb_hd) * 1.00001f + (float)(Mpass * 1e-6);
             const float R2s = rv < 0.0f ? -1.0f : Rs * Rs;
 #pragma unroll
@@ -613,15 +572,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
                                 lo2 = b0 + 1;
                                 hi2 = b1;
                             }
-                            const long long rowbase = ((long long)ccz * g.nc[1] + ccy) * g.nc[0];
-                            if (lo1 <= hi1) {
-                                rs[2 * q] = cstart[rowbase + lo1];
-                                rc[2 * q] = (int)(cstart[rowbase + hi1 + 1] - rs[2 * q]);
-                            }
-                            if (lo2 <= hi2) {
-                                rs[2 * q + 1] = cstart[rowbase + lo2];
-                                rc[2 * q + 1] = (int)(cstart[rowbase + hi2 + 1] - rs[2 * q + 1]);
-                            }
+                            // both runs' bounds in flight together (an empty run reads cell 0 twice)
+                            const uint32_t *rp = cstart + ((long long)ccz * g.nc[1] + ccy) * g.nc[0];
+                            const bool e1 = lo1 <= hi1, e2 = lo2 <= hi2;
+                            const uint32_t s1 = rp[e1 ? lo1 : 0], t1 = rp[e1 ? hi1 + 1 : 0];
+                            const uint32_t s2 = rp[e2 ? lo2 : 0], t2 = rp[e2 ? hi2 + 1 : 0];
+                            rs[2 * q] = s1;
+                            rc[2 * q] = (int)(t1 - s1);
+                            rs[2 * q + 1] = s2;
+                            rc[2 * q + 1] = (int)(t2 - s2);
                             ++n_rows;
                         }
                     }
@@ -729,15 +688,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
         if (a.kd_recs != nullptr) {
             // the k-NN records (list order) seed the next finer level's tiles
             double4 *o = a.kd_recs + vo * (size_t)a.k;
+            double4 rec[KMAX];
+#pragma unroll
+            for (int j = 0; j < KMAX; ++j) rec[j] = prec[max(bp[j], 0)];  // every load in flight at once
 #pragma unroll
             for (int j = 0; j < KMAX; ++j) {
                 if (j >= a.kpad) {
-                    double4 r = make_double4(0.0, 0.0, 0.0, __longlong_as_double(-1LL));
-                    if (bp[j] >= 0) {
-                        r = prec[bp[j]];
-                        r.w = __longlong_as_double((long long)bp[j]);
-                    }
-                    o[j - a.kpad] = r;
+                    const bool ok = bp[j] >= 0;
+                    o[j - a.kpad] = make_double4(ok ? rec[j].x : 0.0, ok ? rec[j].y : 0.0, ok ? rec[j].z : 0.0,
+                                                 __longlong_as_double((long long)bp[j]));
                 }
             }
         }
@@ -771,6 +730,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
         }
     }
     const int k = a.k;
+    // the neighbours' value records: every load issued here, before the weight arithmetic
+    // below, so their latency overlaps it (slots past k are clamped to a valid record)
+    double pvu[KMAX], pvv[KMAX], pvw[KMAX];
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) {
+        const double4 r = pval[max(bp[j], 0)];
+        pvu[j] = r.x;
+        pvv[j] = r.y;
+        pvw[j] = r.z;
+    }
     double w[KMAX];
     if (a.method == PTV_METHOD_SIBSON) {
         // interpolator.py:106-116
@@ -808,13 +777,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
     }
 
     // interpolator.py:150-153: per component, sum_k w * values[idx, c]
-    const double *vb = reinterpret_cast<const double *>(pval);
     double out[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         double t[KMAX];
 #pragma unroll
-        for (int j = 0; j < KMAX; ++j) t[j] = (j < k) ? w[j] * vb[(size_t)max(bp[j], 0) * 4 + c] : 0.0;
+        for (int j = 0; j < KMAX; ++j) t[j] = (j < k) ? w[j] * (c == 0 ? pvu[j] : (c == 1 ? pvv[j] : pvw[j])) : 0.0;
         out[c] = pairwise<KMAX>(t, k);
     }
     if (a.flags & PTV_FLAG_NAN_TO_NUM) {
@@ -876,9 +844,7 @@ __device__ __forceinline__ int count_inside(const CellGrid &g, const uint32_t *_
         const long long base = ((long long)ccz * g.nc[1] + ccy) * g.nc[0];
         cnt += (int)(cstart[base + bb + 1] - cstart[base + aa]);
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
-    return cnt;
+    return group_reduce<0x3f>(cnt, OpAdd{});
 }
 
 __global__ __launch_bounds__(256) void k_count_bound(CellGrid g, const uint32_t *__restrict__ cstart,
