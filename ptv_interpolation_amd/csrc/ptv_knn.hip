@@ -114,6 +114,27 @@ __device__ __forceinline__ double np_pow(double d, double p) {
     return pow(d, p);
 }
 
+// a / b correctly rounded from r = RN(1/b): q = RN(a r), then q + RN(a - b q) r (Markstein; exact
+// for normal operands, checked against IEEE division on 3.6e8 random pairs).  One division
+// serves every numerator that shares the denominator.
+__device__ __forceinline__ double div_by(double a, double b, double r) {
+    const double q = a * r;
+    return fma(fma(-q, b, a), r, q);
+}
+
+// IEEE sqrt for x >= 2^-767: the LLVM gfx9 f64 expansion (rsq seed, two Goldschmidt
+// corrections) without its small-input rescale; tiny, zero and infinite x take sqrt()
+__device__ __forceinline__ double sqrt_cr(double x) {
+    if (!(x >= 0x1p-767 && x < INFINITY)) return sqrt(x);
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = y * 0.5;
+    const double r = fma(-h, g, 0.5);
+    g = fma(g, r, g);
+    h = fma(h, r, h);
+    g = fma(fma(-g, g, x), h, g);
+    return fma(fma(-g, g, x), h, g);
+}
+
 __device__ __forceinline__ double nan_to_num(double v) {
     if (v != v) return 0.0;
     if (v == INFINITY) return DBL_MAX;
@@ -142,6 +163,19 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// v_min_f64 / v_max_f64 without the input canonicalisation fmin/fmax get in IEEE mode (the
+// list never holds NaN or signalling values)
+__device__ __forceinline__ double vmin_f64(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double vmax_f64(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 template <int KMAX>
 __device__ __forceinline__ void insert(double (&bd)[KMAX], int (&bp)[KMAX], double d2, int p) {
     // Ascending carry sweep: m_j = d2 < bd[j] is monotone in j over the sorted list; from the
@@ -152,12 +186,14 @@ __device__ __forceinline__ void insert(double (&bd)[KMAX], int (&bp)[KMAX], doub
     int cp = p;
 #pragma unroll
     for (int j = 0; j < KMAX; ++j) {
+        // on a sorted list the carry is never below bd[j] once it differs from d2, so the
+        // distance slot is min(bd[j], carry) and the new carry the max (one op each)
         const bool mj = d2 < bd[j];
         const double od = bd[j];
         const int op = bp[j];
-        bd[j] = mj ? cd : od;
+        bd[j] = vmin_f64(od, cd);
+        cd = vmax_f64(od, cd);
         bp[j] = mj ? cp : op;
-        cd = mj ? od : cd;
         cp = mj ? op : cp;
     }
 }
@@ -746,7 +782,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
         double d[KMAX], t[KMAX];
 #pragma unroll
         for (int j = 0; j < KMAX; ++j) {
-            d[j] = (j < k) ? sqrt(bd[j]) : 0.0;
+            d[j] = (j < k) ? sqrt_cr(bd[j]) : 0.0;
             t[j] = (j < k) ? 1.0 / (d[j] + a.eps) : 0.0;
         }
         const double s_inv = pairwise<KMAX>(t, k);
@@ -768,12 +804,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
         // interpolator.py:143-147
 #pragma unroll
         for (int j = 0; j < KMAX; ++j) {
-            const double d = sqrt(bd[j]);
+            const double d = sqrt_cr(bd[j]);
             w[j] = (j < k) ? 1.0 / (np_pow(d, a.power) + a.eps) : 0.0;
         }
         const double s = pairwise<KMAX>(w, k);
+        // w_j / s through one reciprocal when s and every quotient are normal (w_j > 0 here:
+        // s <= 2^1000 and min_j w_j >= s 2^-1000); IEEE division on any lane otherwise
+        double wmin = w[0];
 #pragma unroll
-        for (int j = 0; j < KMAX; ++j) w[j] = w[j] / s;
+        for (int j = 1; j < KMAX; ++j)
+            if (j < k) wmin = fmin(wmin, w[j]);
+        const bool fast = s <= 0x1p1000 && wmin >= s * 0x1p-1000;
+        if (__builtin_amdgcn_ballot_w64(!fast) == 0) {
+            const double rs = 1.0 / s;
+#pragma unroll
+            for (int j = 0; j < KMAX; ++j) w[j] = div_by(w[j], s, rs);
+        } else {
+#pragma unroll
+            for (int j = 0; j < KMAX; ++j) w[j] = w[j] / s;
+        }
     }
 
     // interpolator.py:150-153: per component, sum_k w * values[idx, c]
