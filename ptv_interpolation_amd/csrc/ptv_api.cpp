@@ -183,7 +183,11 @@ int ptv_free(ptv_ctx *c) {
 
 namespace {
 
-constexpr double kDefaultOccupancy = 1.2;  // particles per binning cell
+// particles per binning cell: the k <= 8 kernels (seeded, sub-ball filtered copy) are fastest
+// with coarse cells (fewer, longer runs per row: 512^3 / 5M k=8 main launch 19.1 -> 16.5 ms
+// from 1.2 to 5.5); the larger-k kernels prefer fine cells (k=50: 477 ms at 1.2, 493 at 5.5)
+constexpr double kDefaultOccupancySmallK = 5.5;
+constexpr double kDefaultOccupancy = 1.2;
 constexpr double kDefaultR0Scale = 1.0;     // first gather radius / expected k-NN radius
 constexpr long long kMaxCells = 1LL << 28;
 constexpr long long kLatticeStopPoints = 50000; // no coarser lattice below this many points
@@ -250,6 +254,7 @@ CellGrid make_cell_grid(const double lo_in[3], const double hi_in[3], int64_t n,
         maxabs = std::max(maxabs, std::max(std::fabs(lo_in[a]), std::fabs(hi_in[a])));
     }
     if (!(occ > 0.0)) occ = kDefaultOccupancy;
+    if (const char *e = std::getenv("PTV_CELL_OCC")) occ = std::atof(e);  // dev override
     double vol = 1.0;
     int dims = 0;
     for (int a = 0; a < 3; ++a)
@@ -350,7 +355,9 @@ int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchP
     }
 
     // 2. binning
-    CellGrid cg = make_cell_grid(lo, hi, n, prm->cell_occupancy);
+    const double occ = prm->cell_occupancy > 0.0 ? prm->cell_occupancy
+                       : (kmax_for(prm->k) <= 8 ? kDefaultOccupancySmallK : kDefaultOccupancy);
+    CellGrid cg = make_cell_grid(lo, hi, n, occ);
     const size_t m = (size_t)cg.ncells;
     PTV_TRY(c->code.ensure(n));
     PTV_TRY(c->perm.ensure(n));

@@ -34,6 +34,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
+#include <cstdlib>
+#include <algorithm>
 #include <cmath>
 
 #include "../../include/ptv_api.h"
@@ -68,6 +70,7 @@ struct KnnKernelArgs {
     double4 *kd_recs;  // kModeKDist: k-NN particle records out (NULL = none)
     int lz0;           // plane of coarse-lattice point 0
     uint32_t *slots;   // kModeSlots: neighbour slots out
+    int seed_n;        // seed records used per lattice corner (<= k)
 };
 
 // numpy pairwise sum of a[0..n) (n <= KMAX <= 128), from identity 0.0.
@@ -305,7 +308,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
             const int jx = min(jx0 + (cc & 1), a.cb.n[0] - 1);
             const int jy = min(jy0 + ((cc >> 1) & 1), a.cb.n[1] - 1);
             const int jz = min(jz0 + (cc >> 2), a.cb.n[2] - 1);
-            if (j < a.k) seed = a.cb.recs[(((size_t)jz * a.cb.n[1] + jy) * a.cb.n[0] + jx) * a.k + j];
+            if (j < a.seed_n) seed = a.cb.recs[(((size_t)jz * a.cb.n[1] + jy) * a.cb.n[0] + jx) * a.k + j];
         }
     }
 
@@ -1006,6 +1009,8 @@ int launch_knn(const KnnLaunch &a, const Binned &b, const double *ax, const doub
     ka.kd_recs = a.kd_recs;
     ka.lz0 = a.lz0 < 0 ? a.z0 : a.lz0;
     ka.slots = a.slots;
+    ka.seed_n = a.k;
+    if (const char *e = std::getenv("PTV_SEED_N")) ka.seed_n = std::max(1, std::min(a.k, std::atoi(e)));  // dev knob
     if (a.mode == kModeSlots && (a.slots == nullptr || (a.z0 - ka.lz0) % 4 != 0)) {
         set_error("slot-mode k-NN launch needs an output buffer and a tile-aligned first plane");
         return PTV_E_ARG;

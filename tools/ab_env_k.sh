@@ -1,0 +1,11 @@
+#!/bin/bash
+# A/B a dev environment knob on a bench variant: tools/ab_env_k.sh "BENCH ARGS" VAR v1 v2 ...
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
+mkdir -p gpurun_out
+args=$1; shift
+var=$1; shift
+for v in "$@"; do
+  env "$var=$v" timeout -k 10 200 python bench.py $args --steps 3 --warmup 1 --no-cpu-baseline > "gpurun_out/ab_$v.log" 2>&1 || { tail -5 "gpurun_out/ab_$v.log"; exit 1; }
+  python3 -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);print(sys.argv[2], d['breakdown_ms'], d['ms_per_step'])" "gpurun_out/ab_$v.log" "$var=$v"
+done
