@@ -386,7 +386,9 @@ int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchP
         const double *src[3] = {ax, ay, az + z0};
         while (nlat < kMaxLattice) {
             const long long pts = (long long)n[0] * n[1] * n[2];
-            if (pts <= kLatticeStopPoints || std::min(n[0], std::min(n[1], n[2])) < 9) break;
+            long long stop = kLatticeStopPoints;
+            if (const char *e = std::getenv("PTV_LAT_STOP")) stop = std::atoll(e);  // dev override
+            if (pts <= stop || std::min(n[0], std::min(n[1], n[2])) < 9) break;
             Lat &L = lat[nlat];
             for (int d = 0; d < 3; ++d) L.n[d] = n[d] <= 1 ? 1 : (n[d] - 1 + kLatticeStep - 1) / kLatticeStep + 1;
             PTV_TRY(c->lat_axes[nlat].ensure((size_t)L.n[0] + L.n[1] + L.n[2]));
