@@ -638,11 +638,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
                 }
                 wave_lds_sync();
                 stamp(t_rows);
-                for (int src = 0; src < total; src += 64) {
-                    // ---- copy window [src, src + 64) of this round's candidates.  Each run marks its
-                    //      first window position with its id (ids grow with candidate order), a prefix
-                    //      max gives every lane its run; lane i loads candidate src + i and keeps it
-                    //      only if it lies in some sub-ball (compacted into the LDS buffer) ----
+                // ---- copy windows [src, src + 64) of this round's candidates.  Each run marks its
+                //      first window position with its id (ids grow with candidate order), a prefix
+                //      max gives every lane its run; lane i takes candidate src + i and keeps it
+                //      only if it lies in some sub-ball (compacted into the LDS buffer).  Software
+                //      pipelined: the next window's records are in flight while this one is filtered.
+                auto window_slot = [&](int src) -> uint32_t {
                     owner[lane] = -1;
                     wave_lds_sync();
 #pragma unroll
@@ -653,15 +654,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
                     }
                     wave_lds_sync();
                     const int o = wave_incl_max_scan_i(owner[lane]);
+                    uint32_t sl = 0;  // lanes past the end read record 0 and drop it
+                    if (src + lane < total) {
+                        const uint2 rn = runs[o];
+                        sl = rn.y + (uint32_t)(src + lane - (int)rn.x);
+                    }
+                    return sl;
+                };
+                uint32_t next_slot = total > 0 ? window_slot(0) : 0u;
+                double4 next_rec = prec[next_slot];
+                for (int src = 0; src < total; src += 64) {
+                    const uint32_t slot = next_slot;
+                    const double4 p4 = next_rec;
+                    if (src + 64 < total) {
+                        next_slot = window_slot(src + 64);
+                        next_rec = prec[next_slot];
+                    }
                     const int i = src + lane;
                     bool keep = false;
-                    double4 p4 = make_double4(0.0, 0.0, 0.0, 0.0);
-                    uint32_t slot = 0;
                     float ex = 0.f, ey = 0.f, ez = 0.f;
                     if (i < total) {
-                        const uint2 rn = runs[o];
-                        slot = rn.y + (uint32_t)(i - (int)rn.x);
-                        p4 = prec[slot];
                         ex = (float)(p4.x - tcx);
                         ey = (float)(p4.y - tcy);
                         ez = (float)(p4.z - tcz);
