@@ -108,6 +108,43 @@ __device__ __forceinline__ double pairwise(const double (&a)[KMAX], int n) {
     return 0.0;
 }
 
+// numpy pairwise sum of t[j] = w[j] * values[bp[j], c] over j < n (n >= 1), streaming the
+// value loads in blocks of 8 (one block in flight at a time) instead of holding KMAX of them.
+// Same order as pairwise(): 8 accumulators seeded with t[0..7], blocks of 8, then the tail.
+template <int KMAX>
+__device__ __forceinline__ double gather_pairwise(const double (&w)[KMAX], const int (&bp)[KMAX],
+                                                  const double *__restrict__ vb, int c, int n) {
+    auto val = [&](int j) { return vb[(size_t)max(bp[j], 0) * 4 + c]; };
+    double v8[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v8[i] = val(i);
+    if (n < 8) {
+        double r = 0.0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            if (i < n) r += w[i] * v8[i];
+        return r;
+    }
+    double r[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r[i] = w[i] * v8[i];
+    const int stop = n - (n & 7);
+#pragma unroll
+    for (int m = 8; m + 8 <= KMAX; m += 8) {
+        if (m < stop) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v8[i] = val(m + i);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) r[i] += w[m + i] * v8[i];
+        }
+    }
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+#pragma unroll
+    for (int j = 8; j < KMAX; ++j)
+        if (j >= stop && j < n) res += w[j] * val(j);
+    return res;
+}
+
 // d ** p with numpy's scalar fast paths (p uniform).
 __device__ __forceinline__ double np_pow(double d, double p) {
     if (p == 2.0) return d * d;
@@ -781,11 +818,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
         }
     }
     const int k = a.k;
-    // the neighbours' value records: every load issued here, before the weight arithmetic
-    // below, so their latency overlaps it (slots past k are clamped to a valid record)
-    double pvu[KMAX], pvv[KMAX], pvw[KMAX];
+    // k <= 8: the neighbours' value records are all loaded here, before the weight
+    // arithmetic below, so their latency overlaps it (slots past k are clamped to a valid
+    // record).  Larger lists stream them per component after the weights (register budget).
+    constexpr int KV = KMAX <= 8 ? KMAX : 1;
+    double pvu[KV], pvv[KV], pvw[KV];
 #pragma unroll
-    for (int j = 0; j < KMAX; ++j) {
+    for (int j = 0; j < KV; ++j) {
         const double4 r = pval[max(bp[j], 0)];
         pvu[j] = r.x;
         pvv[j] = r.y;
@@ -842,12 +881,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
 
     // interpolator.py:150-153: per component, sum_k w * values[idx, c]
     double out[3];
+    if constexpr (KMAX <= 8) {
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        double t[KMAX];
+        for (int c = 0; c < 3; ++c) {
+            double t[KMAX];
 #pragma unroll
-        for (int j = 0; j < KMAX; ++j) t[j] = (j < k) ? w[j] * (c == 0 ? pvu[j] : (c == 1 ? pvv[j] : pvw[j])) : 0.0;
-        out[c] = pairwise<KMAX>(t, k);
+            for (int j = 0; j < KMAX; ++j) t[j] = (j < k) ? w[j] * (c == 0 ? pvu[j] : (c == 1 ? pvv[j] : pvw[j])) : 0.0;
+            out[c] = pairwise<KMAX>(t, k);
+        }
+    } else {
+        const double *vb = reinterpret_cast<const double *>(pval);
+#pragma unroll 1
+        for (int c = 0; c < 3; ++c) out[c] = gather_pairwise<KMAX>(w, bp, vb, c, k);
     }
     if (a.flags & PTV_FLAG_NAN_TO_NUM) {
 #pragma unroll
