@@ -42,6 +42,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "Mvoxels/s interpolated + achieved HBM GB/s, 512³ grid / 5M particles IDW"
+METRIC_DIV = "Mvoxels/s + achieved HBM GB/s, consistent divergence (physics.py:6-53) of a 512³ field"
 METRIC_RBF = "Mvoxels/s interpolated + achieved FP64 TFLOP/s, 512³ grid / 5M particles local RBF"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec (AMD); not listed in the guide
@@ -74,7 +75,9 @@ def parse():
     ap.add_argument("--particles", type=int, default=5_000_000)
     ap.add_argument("--k", type=int, default=8)
     ap.add_argument("--power", type=float, default=2.0)
-    ap.add_argument("--method", default="idw", choices=["idw", "sibson", "rbf"])
+    ap.add_argument("--method", default="idw", choices=["idw", "sibson", "nearest", "rbf", "div"])
+    ap.add_argument("--div-dtype", default="f64", choices=["f64", "f32"],
+                    help="--method div: field dtype (f32 = the C5 fp32 field, Python-float spacings)")
     ap.add_argument("--rbf-kernel", default="thin_plate_spline", help="--method rbf: scipy kernel name")
     ap.add_argument("--epsilon", type=float, default=None, help="--method rbf: shape parameter")
     ap.add_argument("--degree", type=int, default=None, help="--method rbf: polynomial degree")
@@ -168,8 +171,123 @@ def cpu_baseline_rbf(args, P, Q, ax):
             "seconds": round(dt, 2)}
 
 
+def cpu_baseline_div(args, fields, fluid):
+    """Oracle divergence (numpy, one process — the reference's physics.py is single-threaded
+    numpy) on a bounded z-slab sample of the same field."""
+    from oracle import cpu_ref
+
+    G = args.grid
+    planes = min(64, G)
+    sl = slice(G // 2 - planes // 2, G // 2 - planes // 2 + planes)
+    u, v, w = (f[sl] for f in fields)
+    t = time.perf_counter()
+    cpu_ref.consistent_divergence(u, v, w, fluid[sl], 1.0, 1.0, 1.0)
+    dt = time.perf_counter() - t
+    nvox = planes * G * G
+    return {"value": round(nvox / dt / 1e6, 3), "unit": "Mvoxels/s", "cores": 1, "kind": "port",
+            "sample": f"{planes} central z-planes ({nvox} voxels) of the same {G}^3 field; numpy restatement "
+                      f"of physics.compute_consistent_divergence (oracle/cpu_ref.py), 1 process",
+            "seconds": round(dt, 2)}
+
+
+def main_div(args):
+    """--method div: one step = the consistent divergence of a resident (G, G, G) velocity field
+    with the sphere-pack fluid mask (view_divergence.py:39).  Weak scaling: each rank owns a
+    G^3 z-slab plus one halo plane per interior side (no collective on the data path)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+
+    dist = None
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    from ptv_interpolation_amd import _lib, synth
+
+    G = args.grid
+    f32 = args.div_dtype == "f32"
+    tdt = torch.float32 if f32 else torch.float64
+    s = 4 if f32 else 8
+    lo = 1 if rank > 0 else 0
+    hi = 1 if rank < world - 1 else 0
+    nzb = G + lo + hi
+    fluid = synth.fluid_mask(G)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1234 + rank)
+    fields = [torch.randn((nzb, G, G), generator=gen, dtype=tdt, device=dev) for _ in range(3)]
+    mask_np = np.concatenate([fluid[-lo:] if lo else fluid[:0], fluid, fluid[:hi]])
+    mask = torch.from_numpy(np.ascontiguousarray(mask_np).view(np.uint8)).to(dev)
+    out = torch.empty((G, G, G), dtype=tdt, device=dev)
+    ctx = _lib.Context(local)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    dtc = _lib.F32 if f32 else _lib.F64
+
+    def step():
+        return ctx.divergence_dev(G, G, nzb, [f.data_ptr() for f in fields], mask.data_ptr(), out.data_ptr(),
+                                  1.0, 1.0, 1.0, field_dtype=dtc, result_dtype=dtc, z_range=(lo, lo + G),
+                                  edges=(lo == 0, hi == 0), stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    k_ms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        k_ms.append(ctx.last_stats()["ms_stencil"])
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    vox = G ** 3
+    kavg = float(np.mean(k_ms))
+    alg = vox * (3 * s + 1 + s)
+    ach = alg / (kavg * 1e-3) / 1e9
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline_div(args, [f.cpu().numpy() for f in fields], fluid)
+        except Exception as e:
+            cpu = {"value": None, "error": repr(e)[:200]}
+    if rank == 0:
+        line = {
+            "metric": METRIC_DIV, "value": round(vox * world / (elapsed / args.steps) / 1e6, 2),
+            "unit": "Mvoxels/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": args.div_dtype,
+            "data": "synthetic: N(0,1) velocity field, generate_sphere_pack.py fluid mask at voxel centres",
+            "config": {"workload": f"consistent divergence of a {G}^3 {args.div_dtype} field (z-slab per GPU)",
+                       "grid": G, "method": "div", "parallelism": f"z-slab x{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
+                         "kernel": f"k_divergence<{'float' if f32 else 'double'}>",
+                         "alg_bytes_per_launch": alg, "kernel_ms": round(kavg, 4)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.method == "div":
+        return main_div(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -199,7 +317,9 @@ def main():
     axes = [torch.from_numpy(ax_h).to(dev), torch.from_numpy(ax_h.copy()).to(dev), torch.from_numpy(az_h).to(dev)]
     out = [torch.empty((G, G, G), dtype=torch.float64, device=dev) for _ in range(3)]
     ctx = _lib.Context(local)
-    method = _lib.METHOD_IDW if args.method == "idw" else _lib.METHOD_SIBSON
+    method = {"idw": _lib.METHOD_IDW, "sibson": _lib.METHOD_SIBSON, "nearest": _lib.METHOD_NEAREST}.get(args.method)
+    if args.method == "nearest":
+        args.k = 1
     stream = torch.cuda.current_stream(dev).cuda_stream
 
     if args.method == "rbf":

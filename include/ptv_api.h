@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define PTV_API_VERSION 2
+#define PTV_API_VERSION 3
 
 /* error codes */
 #define PTV_OK 0
@@ -129,12 +129,37 @@ typedef struct {
     double r0;
     double ms_solve;     /* local RBF: the per-voxel solve kernels (ms_knn = their k-NN passes) */
     int64_t n_singular;  /* local RBF: voxels whose system had an exactly zero pivot */
+    double ms_stencil;   /* ptv_divergence*: the stencil kernel */
 } ptv_stats;
+
+/*
+ * Consistent divergence (physics.compute_consistent_divergence, physics.py:6-53).
+ * Fields U, V, W and the uint8 fluid mask (nonzero = fluid, required: the reference
+ * np.roll()s it, physics.py:31-32) are (nz, ny, nx) C order.  Planes [z_begin, z_end)
+ * are written to `out` as (z_end - z_begin, ny, nx).  Plane 0 / nz-1 of the buffer is
+ * a domain z edge when edge_lo / edge_hi is set, else a one-plane halo of the
+ * neighbouring z-slab that is read but not computed (z-slab multi-GPU).
+ * Types follow numpy: field_dtype is the fields' dtype; result_dtype the dtype of
+ * (field difference) / spacing — PTV_F32 only for float32 fields with Python-float
+ * spacings, PTV_F64 when a spacing is a numpy float64 scalar (view_divergence.py:22).
+ */
+#define PTV_F64 0
+#define PTV_F32 1
+typedef struct {
+    int64_t nx, ny, nz;
+    int64_t z_begin, z_end;
+    int edge_lo, edge_hi;
+    int field_dtype;     /* PTV_F64 | PTV_F32 */
+    int result_dtype;    /* PTV_F64 | PTV_F32 */
+    double dx, dy, dz;
+    const uint8_t *fluid_mask;
+} ptv_div_params;
 
 /* Library / device management. */
 int ptv_version(void);
-/* sizeof(ptv_particles, ptv_grid, ptv_knn_params, ptv_stats, ptv_rbf_params): binding self-check */
-int ptv_abi_sizes(int64_t out5[5]);
+/* sizeof(ptv_particles, ptv_grid, ptv_knn_params, ptv_stats, ptv_rbf_params, ptv_div_params):
+ * binding self-check */
+int ptv_abi_sizes(int64_t out6[6]);
 const char *ptv_last_error(void);
 int ptv_device_count(int *out);
 int ptv_init(int device, ptv_ctx **out);
@@ -180,6 +205,18 @@ int ptv_interp_rbf_local(ptv_ctx *ctx, const ptv_particles *p, const ptv_grid *g
 int ptv_interp_rbf_local_dev(ptv_ctx *ctx, const ptv_particles *p, const ptv_grid *g,
                              const ptv_rbf_params *prm, double *U, double *V, double *W,
                              void *stream, ptv_stats *st);
+
+/*
+ * Consistent divergence, host buffers: H2D of the fields and mask, one stencil kernel,
+ * D2H of the slab.  Replaces compute_consistent_divergence(u, v, w, mask, dx, dy, dz)
+ * (physics.py:6-53; callers view_divergence.py:39,42, physics.py:173,193-194).
+ */
+int ptv_divergence(ptv_ctx *ctx, const ptv_div_params *prm, const void *U, const void *V,
+                   const void *W, void *out, ptv_stats *st);
+
+/* Same on device pointers (fields, mask, out), enqueued on `stream` (NULL = ctx's). */
+int ptv_divergence_dev(ptv_ctx *ctx, const ptv_div_params *prm, const void *U, const void *V,
+                       const void *W, void *out, void *stream, ptv_stats *st);
 
 /*
  * Last-launch k-NN kernel duration in ms (hipEvent pair recorded around the

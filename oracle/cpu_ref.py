@@ -13,6 +13,11 @@ What it restates (reference = tombultreys/ptv_interpolation, read-only):
   through scipy's ``RBFInterpolator(neighbors=k)`` evaluation
   (``_rbfinterp.py:463-556``, ``_build_system`` / ``dgesv`` :82-127): see
   ``rbf_local_points`` below
+* ``interpolate_field(method='nearest')`` (interpolator.py:196-197: griddata ->
+  NearestNDInterpolator, a k=1 KDTree query, values[idx]) in ``interp_points``
+* ``physics.compute_consistent_divergence`` (physics.py:6-53) as
+  ``consistent_divergence`` below (an independent per-axis index restatement,
+  not the reference's np.roll formulation)
 * the RBF process fan-out pattern (interpolator.py:173-182,
   test_parallel.py:6-28) as a z-slab ``ProcessPoolExecutor`` driver used as the
   same-box CPU baseline.
@@ -165,10 +170,15 @@ def interp_points(points, values, queries, method="idw", k=8, power=2.0, knn="kd
     points = np.asarray(points, dtype=np.float64)
     values = np.asarray(values, dtype=np.float64)
     queries = np.asarray(queries, dtype=np.float64).reshape(-1, 3)
+    if method == "nearest":
+        k = 1
     if knn == "kdtree":
         dist, idx = knn_kdtree(points, queries, k)
     else:
         dist, idx = knn_bruteforce(points, queries, k)
+    if method == "nearest":
+        # NearestNDInterpolator.__call__: values[i] for the single nearest particle
+        return values[np.asarray(idx).reshape(-1)]
     if method == "idw":
         w = idw_weights(dist, power)
     elif method == "sibson":
@@ -353,3 +363,32 @@ def nan_fill_and_mask(U, V, W, fluid_mask=None):
         V[solid] = 0
         W[solid] = 0
     return U, V, W
+
+
+# ----------------------------------------------------------------------------
+# consistent divergence (physics.py:6-53)
+# ----------------------------------------------------------------------------
+def _faces(vel, fluid, axis):
+    """(f_next, f_prev) of get_face_vel (physics.py:26-48) along ``axis``, by index:
+    f_next[i] = (vel[i] + vel[i+1]) / 2 if fluid[i+1] else 0, = vel[i] at i = n-1;
+    f_prev[i] = f_next[i-1] = (vel[i-1] + vel[i]) / 2 if fluid[i] else 0, = vel[i] at i = 0."""
+    v = np.moveaxis(vel, axis, -1)
+    m = np.moveaxis(fluid, axis, -1)
+    zero = np.zeros((), dtype=vel.dtype)
+    fn = np.empty_like(v)
+    fp = np.empty_like(v)
+    fn[..., :-1] = np.where(m[..., 1:], (v[..., :-1] + v[..., 1:]) / 2.0, zero)
+    fn[..., -1] = v[..., -1]
+    fp[..., 1:] = np.where(m[..., 1:], (v[..., :-1] + v[..., 1:]) / 2.0, zero)
+    fp[..., 0] = v[..., 0]
+    return np.moveaxis(fn, -1, axis), np.moveaxis(fp, -1, axis)
+
+
+def consistent_divergence(u, v, w, mask, dx, dy, dz):
+    """div = ((ufn - ufp)/dx + (vfn - vfp)/dy) + (wfn - wfp)/dz (physics.py:53), numpy's
+    evaluation order and dtype promotion (the spacing scalars are passed through as given)."""
+    fluid = np.asarray(mask).astype(bool)
+    ufn, ufp = _faces(np.asarray(u), fluid, 2)
+    vfn, vfp = _faces(np.asarray(v), fluid, 1)
+    wfn, wfp = _faces(np.asarray(w), fluid, 0)
+    return (ufn - ufp) / dx + (vfn - vfp) / dy + (wfn - wfp) / dz

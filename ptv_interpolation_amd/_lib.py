@@ -67,12 +67,24 @@ class RbfParams(C.Structure):
                 ("flags", C.c_uint32), ("chunk_planes", C.c_int)]
 
 
+F64 = 0
+F32 = 1
+
+
+class DivParams(C.Structure):
+    _fields_ = [("nx", C.c_int64), ("ny", C.c_int64), ("nz", C.c_int64), ("z_begin", C.c_int64),
+                ("z_end", C.c_int64), ("edge_lo", C.c_int), ("edge_hi", C.c_int), ("field_dtype", C.c_int),
+                ("result_dtype", C.c_int), ("dx", C.c_double), ("dy", C.c_double), ("dz", C.c_double),
+                ("fluid_mask", C.POINTER(C.c_uint8))]
+
+
 class Stats(C.Structure):
     _fields_ = [("ms_h2d", C.c_double), ("ms_bin", C.c_double), ("ms_lattice", C.c_double), ("ms_knn", C.c_double),
                 ("ms_d2h", C.c_double),
                 ("ms_total", C.c_double), ("n_particles", C.c_int64), ("n_voxels", C.c_int64),
                 ("n_cells", C.c_int64), ("cells", C.c_int32 * 3), ("cell_size", C.c_double * 3),
-                ("r0", C.c_double), ("ms_solve", C.c_double), ("n_singular", C.c_int64)]
+                ("r0", C.c_double), ("ms_solve", C.c_double), ("n_singular", C.c_int64),
+                ("ms_stencil", C.c_double)]
 
     def as_dict(self):
         d = {f: getattr(self, f) for f, _ in self._fields_}
@@ -96,6 +108,10 @@ EXPORTS = {
                                        _dp, _dp, _dp, C.POINTER(Stats)]),
     "ptv_interp_rbf_local_dev": (C.c_int, [C.c_void_p, C.POINTER(Particles), C.POINTER(Grid),
                                            C.POINTER(RbfParams), _dp, _dp, _dp, C.c_void_p, C.POINTER(Stats)]),
+    "ptv_divergence": (C.c_int, [C.c_void_p, C.POINTER(DivParams), C.c_void_p, C.c_void_p, C.c_void_p,
+                                 C.c_void_p, C.POINTER(Stats)]),
+    "ptv_divergence_dev": (C.c_int, [C.c_void_p, C.POINTER(DivParams), C.c_void_p, C.c_void_p, C.c_void_p,
+                                     C.c_void_p, C.c_void_p, C.POINTER(Stats)]),
     "ptv_last_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
     "ptv_debug_stamps": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_double)]),
 }
@@ -146,9 +162,10 @@ def check(rc):
 
 def abi_sizes():
     """(C sizeof, ctypes sizeof) for each ABI struct: they must agree."""
-    out = (C.c_int64 * 5)()
+    out = (C.c_int64 * 6)()
     check(lib().ptv_abi_sizes(out))
-    py = [C.sizeof(Particles), C.sizeof(Grid), C.sizeof(KnnParams), C.sizeof(Stats), C.sizeof(RbfParams)]
+    py = [C.sizeof(Particles), C.sizeof(Grid), C.sizeof(KnnParams), C.sizeof(Stats), C.sizeof(RbfParams),
+          C.sizeof(DivParams)]
     return list(out), py
 
 
@@ -324,4 +341,39 @@ class Context:
         st = Stats()
         check(lib().ptv_interp_knn_dev(self.h, C.byref(P), C.byref(G), C.byref(prm),
                                        *[dev_dp(p) for p in out_ptrs], C.c_void_p(stream or 0), C.byref(st)))
+        return st.as_dict()
+
+    # -- consistent divergence (physics.py:6-53) ---------------------------
+    def divergence(self, u, v, w, fluid_mask, dx, dy, dz, result_dtype=None, z_range=None, edges=(True, True)):
+        """Host-array divergence of (nz, ny, nx) fields; returns (z1 - z0, ny, nx) of
+        ``result_dtype`` (default: the fields' dtype).  ``edges``: whether buffer plane 0 /
+        nz-1 is a domain edge (else a halo plane, read but not computed)."""
+        ft = np.result_type(u.dtype, v.dtype, w.dtype)
+        if ft not in (np.float32, np.float64):
+            ft = np.dtype(np.float64)
+        rt = np.dtype(result_dtype) if result_dtype is not None else np.dtype(ft)
+        f = [np.ascontiguousarray(a, dtype=ft) for a in (u, v, w)]
+        nz, ny, nx = f[0].shape
+        mk = np.ascontiguousarray(fluid_mask, dtype=bool).view(np.uint8).reshape(nz, ny, nx)
+        z0, z1 = (0, nz) if z_range is None else z_range
+        prm = DivParams(nx, ny, nz, z0, z1, int(bool(edges[0])), int(bool(edges[1])),
+                        F32 if ft == np.float32 else F64, F32 if rt == np.float32 else F64,
+                        float(dx), float(dy), float(dz), mk.ctypes.data_as(C.POINTER(C.c_uint8)))
+        out = np.empty((z1 - z0, ny, nx), dtype=rt)
+        st = Stats()
+        check(lib().ptv_divergence(self.h, C.byref(prm), *[a.ctypes.data_as(C.c_void_p) for a in f],
+                                   out.ctypes.data_as(C.c_void_p), C.byref(st)))
+        self.stats = st.as_dict()
+        return out
+
+    def divergence_dev(self, nx, ny, nz, ptrs, mask_ptr, out_ptr, dx, dy, dz, field_dtype=F64, result_dtype=F64,
+                       z_range=None, edges=(True, True), stream=0):
+        """Device-pointer divergence (fields, mask and output resident in HBM); returns stats."""
+        z0, z1 = (0, nz) if z_range is None else z_range
+        prm = DivParams(nx, ny, nz, z0, z1, int(bool(edges[0])), int(bool(edges[1])), int(field_dtype),
+                        int(result_dtype), float(dx), float(dy), float(dz),
+                        C.cast(C.c_void_p(mask_ptr), C.POINTER(C.c_uint8)) if mask_ptr else None)
+        st = Stats()
+        check(lib().ptv_divergence_dev(self.h, C.byref(prm), *[C.c_void_p(p) for p in ptrs], C.c_void_p(out_ptr),
+                                       C.c_void_p(stream or 0), C.byref(st)))
         return st.as_dict()

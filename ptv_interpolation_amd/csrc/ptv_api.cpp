@@ -71,6 +71,9 @@ struct ptv_ctx {
     DevBuf<uint32_t> slots;                                      // local RBF: chunk k-NN slots
     DevBuf<int> rbf_pw, rbf_status;                              // monomial exponents, singular count
     DevBuf<double> smooth;                                       // per-particle smoothing (host calls)
+    DevBuf<uint8_t> fld[4];                                      // divergence host calls: U, V, W, out
+    hipEvent_t ev_div0 = nullptr, ev_div1 = nullptr;             // around the divergence stencil
+    bool div_pending = false;
     std::vector<hipEvent_t> rbf_ev;                              // 3 per chunk: knn start, solve start, end
     int rbf_chunks = 0;
     double *h_bbox = nullptr;  // pinned, 6 doubles
@@ -87,16 +90,17 @@ extern "C" {
 
 int ptv_version(void) { return PTV_API_VERSION; }
 
-int ptv_abi_sizes(int64_t out5[5]) {
-    if (!out5) {
+int ptv_abi_sizes(int64_t out6[6]) {
+    if (!out6) {
         set_error("ptv_abi_sizes: out is NULL");
         return PTV_E_ARG;
     }
-    out5[0] = (int64_t)sizeof(ptv_particles);
-    out5[1] = (int64_t)sizeof(ptv_grid);
-    out5[2] = (int64_t)sizeof(ptv_knn_params);
-    out5[3] = (int64_t)sizeof(ptv_stats);
-    out5[4] = (int64_t)sizeof(ptv_rbf_params);
+    out6[0] = (int64_t)sizeof(ptv_particles);
+    out6[1] = (int64_t)sizeof(ptv_grid);
+    out6[2] = (int64_t)sizeof(ptv_knn_params);
+    out6[3] = (int64_t)sizeof(ptv_stats);
+    out6[4] = (int64_t)sizeof(ptv_rbf_params);
+    out6[5] = (int64_t)sizeof(ptv_div_params);
     return PTV_OK;
 }
 
@@ -135,6 +139,8 @@ int ptv_init(int device, ptv_ctx **out) {
     PTV_HIP(hipEventCreate(&c->ev_bin0));
     PTV_HIP(hipEventCreate(&c->ev_bin1));
     PTV_HIP(hipEventCreate(&c->ev_lat1));
+    PTV_HIP(hipEventCreate(&c->ev_div0));
+    PTV_HIP(hipEventCreate(&c->ev_div1));
     PTV_HIP(hipHostMalloc(&c->h_bbox, 8 * sizeof(double)));
     *out = c;
     return PTV_OK;
@@ -167,6 +173,9 @@ int ptv_free(ptv_ctx *c) {
     c->rbf_pw.release();
     c->rbf_status.release();
     c->smooth.release();
+    for (auto &b : c->fld) b.release();
+    hipEventDestroy(c->ev_div0);
+    hipEventDestroy(c->ev_div1);
     for (hipEvent_t e : c->rbf_ev) hipEventDestroy(e);
     if (c->h_bbox) hipHostFree(c->h_bbox);
     hipEventDestroy(c->ev_knn0);
@@ -626,8 +635,14 @@ int run_rbf(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_rbf
 }
 
 int finish_timing(ptv_ctx *c) {
-    if (!c->timed_pending) return PTV_OK;
     float ms = 0.f;
+    if (c->div_pending) {
+        PTV_HIP(hipEventSynchronize(c->ev_div1));
+        PTV_HIP(hipEventElapsedTime(&ms, c->ev_div0, c->ev_div1));
+        c->last.ms_stencil = ms;
+        c->div_pending = false;
+    }
+    if (!c->timed_pending) return PTV_OK;
     if (c->rbf_chunks > 0) {
         PTV_HIP(hipEventSynchronize(c->rbf_ev[3 * c->rbf_chunks - 1]));
         double knn = 0.0, solve = 0.0;
@@ -745,6 +760,63 @@ int check_call(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const void
         return PTV_E_ARG;
     }
     PTV_HIP(hipSetDevice(c->device));
+    return PTV_OK;
+}
+
+// ptv_div_params -> DivArgs, with the same checks for the host and device calls.
+int div_args(ptv_ctx *c, const ptv_div_params *prm, const void *U, const void *V, const void *W, const void *out,
+             DivArgs &a) {
+    if (!c || !prm) {
+        set_error("NULL context/params");
+        return PTV_E_ARG;
+    }
+    if (!U || !V || !W || !out || !prm->fluid_mask) {
+        set_error("divergence: NULL field, output or fluid mask");
+        return PTV_E_ARG;
+    }
+    if (prm->nx <= 0 || prm->ny <= 0 || prm->nz <= 0 || prm->nx > (1 << 30) || prm->ny > (1 << 30) ||
+        prm->nz > (1 << 30)) {
+        set_error("divergence: dimensions must be positive");
+        return PTV_E_ARG;
+    }
+    const int64_t lo = prm->edge_lo ? 0 : 1, hi = prm->nz - (prm->edge_hi ? 0 : 1);
+    if (prm->z_begin < lo || prm->z_end > hi || prm->z_begin > prm->z_end) {
+        set_error("divergence: planes [" + std::to_string(prm->z_begin) + ", " + std::to_string(prm->z_end) +
+                  ") must lie in [" + std::to_string(lo) + ", " + std::to_string(hi) +
+                  ") (a non-edge buffer end is a halo plane)");
+        return PTV_E_ARG;
+    }
+    if ((prm->field_dtype != PTV_F64 && prm->field_dtype != PTV_F32) ||
+        (prm->result_dtype != PTV_F64 && prm->result_dtype != PTV_F32)) {
+        set_error("divergence: dtype must be PTV_F64 or PTV_F32");
+        return PTV_E_ARG;
+    }
+    a.nx = (int)prm->nx;
+    a.ny = (int)prm->ny;
+    a.nz = (int)prm->nz;
+    a.z_begin = (int)prm->z_begin;
+    a.z_end = (int)prm->z_end;
+    a.edge_lo = prm->edge_lo ? 1 : 0;
+    a.edge_hi = prm->edge_hi ? 1 : 0;
+    a.field_f32 = prm->field_dtype == PTV_F32;
+    a.result_f32 = prm->result_dtype == PTV_F32;
+    a.dx = prm->dx;
+    a.dy = prm->dy;
+    a.dz = prm->dz;
+    if (!a.field_f32 && a.result_f32) {
+        set_error("divergence: float64 fields cannot give float32 results (numpy promotion)");
+        return PTV_E_ARG;
+    }
+    PTV_HIP(hipSetDevice(c->device));
+    return PTV_OK;
+}
+
+int run_div(ptv_ctx *c, const DivArgs &a, const void *U, const void *V, const void *W, const uint8_t *M, void *out,
+            hipStream_t s) {
+    PTV_HIP(hipEventRecord(c->ev_div0, s));
+    PTV_TRY(launch_divergence(a, U, V, W, M, out, s));
+    PTV_HIP(hipEventRecord(c->ev_div1, s));
+    c->div_pending = true;
     return PTV_OK;
 }
 
@@ -867,6 +939,55 @@ int ptv_debug_stamps(ptv_ctx *c, int mode, double *out) {
             out[1 + nv + f] = mx[f];
         }
     }
+    return PTV_OK;
+}
+
+int ptv_divergence_dev(ptv_ctx *c, const ptv_div_params *prm, const void *U, const void *V, const void *W,
+                       void *out, void *stream, ptv_stats *st) {
+    DivArgs a{};
+    PTV_TRY(div_args(c, prm, U, V, W, out, a));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    PTV_TRY(run_div(c, a, U, V, W, prm->fluid_mask, out, s));
+    c->last.n_voxels = (prm->z_end - prm->z_begin) * prm->nx * prm->ny;
+    if (st) *st = c->last;
+    return PTV_OK;
+}
+
+int ptv_divergence(ptv_ctx *c, const ptv_div_params *prm, const void *U, const void *V, const void *W, void *out,
+                   ptv_stats *st) {
+    DivArgs a{};
+    PTV_TRY(div_args(c, prm, U, V, W, out, a));
+    hipStream_t s = c->stream;
+    EventSet ev;
+    for (hipEvent_t &e : ev.e) PTV_HIP(hipEventCreate(&e));
+    const size_t ts = a.field_f32 ? 4 : 8, rs = a.result_f32 ? 4 : 8;
+    const int64_t nfull = prm->nz * prm->nx * prm->ny;
+    const int64_t nout = (prm->z_end - prm->z_begin) * prm->nx * prm->ny;
+    PTV_HIP(hipEventRecord(ev.e[0], s));
+    const void *src[3] = {U, V, W};
+    for (int i = 0; i < 3; ++i) {
+        PTV_TRY(c->fld[i].ensure(nfull * ts));
+        PTV_HIP(hipMemcpyAsync(c->fld[i].p, src[i], nfull * ts, hipMemcpyHostToDevice, s));
+    }
+    PTV_TRY(c->mask.ensure(nfull));
+    PTV_HIP(hipMemcpyAsync(c->mask.p, prm->fluid_mask, nfull, hipMemcpyHostToDevice, s));
+    PTV_TRY(c->fld[3].ensure(nout * rs));
+    PTV_HIP(hipEventRecord(ev.e[1], s));
+    PTV_TRY(run_div(c, a, c->fld[0].p, c->fld[1].p, c->fld[2].p, c->mask.p, c->fld[3].p, s));
+    PTV_HIP(hipEventRecord(ev.e[2], s));
+    PTV_HIP(hipMemcpyAsync(out, c->fld[3].p, nout * rs, hipMemcpyDeviceToHost, s));
+    PTV_HIP(hipEventRecord(ev.e[3], s));
+    PTV_HIP(hipStreamSynchronize(s));
+    PTV_TRY(finish_timing(c));
+    float h2d = 0.f, d2h = 0.f, tot = 0.f;
+    PTV_HIP(hipEventElapsedTime(&h2d, ev.e[0], ev.e[1]));
+    PTV_HIP(hipEventElapsedTime(&d2h, ev.e[2], ev.e[3]));
+    PTV_HIP(hipEventElapsedTime(&tot, ev.e[0], ev.e[3]));
+    c->last.ms_h2d = h2d;
+    c->last.ms_d2h = d2h;
+    c->last.ms_total = tot;
+    c->last.n_voxels = nout;
+    if (st) *st = c->last;
     return PTV_OK;
 }
 

@@ -71,6 +71,19 @@ int launch_knn(const KnnLaunch &a, const Binned &b, const double *ax, const doub
                const double *qx, const double *qy, const double *qz, const uint8_t *mask, double *U, double *V,
                double *W, hipStream_t s);
 
+// ---- consistent divergence (ptv_div.hip) ----
+struct DivArgs {
+    int nx, ny, nz;          // buffer shape (nz planes, C order)
+    int z_begin, z_end;      // buffer planes computed (output plane 0 = z_begin)
+    int edge_lo, edge_hi;    // buffer plane 0 / nz-1 is a domain z edge (else a halo plane)
+    int field_f32;           // fields are float32 (else float64)
+    int result_f32;          // quotients and sums in float32 (else float64)
+    double dx, dy, dz;
+};
+
+int launch_divergence(const DivArgs &a, const void *U, const void *V, const void *W, const uint8_t *M, void *out,
+                      hipStream_t s);
+
 // ---- local RBF (ptv_rbf.hip) ----
 constexpr int kRbfMaxSystem = 64;  // k + #monomials per voxel system
 

@@ -818,6 +818,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
         }
     }
     const int k = a.k;
+    if (a.method == PTV_METHOD_NEAREST) {
+        // griddata(method='nearest') (interpolator.py:196-197): NearestNDInterpolator returns
+        // values[i] of the single nearest particle (k = 1 query), no arithmetic
+        const double4 r = pval[max(bp[0], 0)];
+        const bool fix = (a.flags & PTV_FLAG_NAN_TO_NUM) != 0;
+        U[vo] = fix ? nan_to_num(r.x) : r.x;
+        V[vo] = fix ? nan_to_num(r.y) : r.y;
+        W[vo] = fix ? nan_to_num(r.z) : r.z;
+        return;
+    }
     // k <= 8: the neighbours' value records are all loaded here, before the weight
     // arithmetic below, so their latency overlaps it (slots past k are clamped to a valid
     // record).  Larger lists stream them per component after the weights (register budget).

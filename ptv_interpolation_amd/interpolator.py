@@ -12,14 +12,15 @@ root ``interpolator.py`` re-exports this module):
     sample_mask_on_grid  interpolator.py:205-238
     extract_boundary_particles  interpolator.py:240-284
 
-``interpolate_field(method='idw'|'sibson')`` runs the k-NN search and the
-weighted average as HIP kernels through the C ABI (include/ptv_api.h).  There is
-no CPU fallback for these methods: a missing library or GPU raises.  Results
-reproduce the reference arithmetic (see ptv_interpolation_amd/csrc/ptv_knn.hip);
-``n_jobs`` is accepted and ignored by the GPU methods (the reference uses it only
-for RBF, interpolator.py:173).  ``linear``/``nearest``/``cubic`` are scipy
-``griddata`` calls in the reference (interpolator.py:196-197) and stay so here
-(outside the accelerated path).
+``interpolate_field(method='idw'|'sibson'|'nearest'|'rbf')`` runs the k-NN search
+and the weighted average (or the local RBF solve) as HIP kernels through the C ABI
+(include/ptv_api.h).  There is no CPU fallback for these methods: a missing library
+or GPU raises.  Results reproduce the reference arithmetic (see
+ptv_interpolation_amd/csrc/ptv_knn.hip); ``n_jobs`` is accepted and ignored by the
+GPU methods (the reference uses it only for RBF, interpolator.py:173).  ``nearest``
+is a scipy ``griddata`` call in the reference (interpolator.py:196-197), i.e. a k = 1
+KDTree query, and runs on the same k-NN kernel here; ``linear``/``cubic`` (Qhull
+Delaunay) stay scipy ``griddata`` calls (outside the accelerated path).
 """
 from __future__ import annotations
 
@@ -167,14 +168,14 @@ def _knn_field(points, values, grid_tuple, method, k, power):
         raise ValueError(f"k must be a positive integer, got {k}")
     if n == 0:
         raise ValueError("no particles to interpolate from")
-    if k == 1:
+    if k == 1 and method != "nearest":
         # the reference's KDTree.query(k=1) squeezes to (V,), then .sum(axis=1) fails
         raise np.exceptions.AxisError("axis 1 is out of bounds for array of dimension 1")
     if k > n:
         # KDTree pads missing neighbours with index n; values[indices] then fails
         raise IndexError(f"index {n} is out of bounds for axis 0 with size {n}")
     ctx = _lib.Context.get(_gpu_device())
-    m = _lib.METHOD_IDW if method == "idw" else _lib.METHOD_SIBSON
+    m = {"idw": _lib.METHOD_IDW, "sibson": _lib.METHOD_SIBSON, "nearest": _lib.METHOD_NEAREST}[method]
     axes = separable_axes(X, Y, Z)
     if axes is not None:
         U, V, W = ctx.interp_knn(points, values, axes=axes, method=m, k=k, power=power, eps=_EPS)
@@ -209,7 +210,11 @@ def interpolate_field(df, grid_tuple, method="linear", rbf_neighbors=20, rbf_ker
 
         return _rbf.rbf_field(points, values, grid_tuple, int(rbf_neighbors), rbf_kernel, smoothing,
                               n_jobs=int(n_jobs))
-    # scattered-data griddata methods: not part of the accelerated path (interpolator.py:196-197)
+    if method == "nearest":
+        # griddata(method='nearest') (interpolator.py:196-197) is NearestNDInterpolator: the
+        # k = 1 query of the same GPU k-NN kernel, values of the nearest particle
+        return _knn_field(points, values, grid_tuple, "nearest", 1, 2.0)
+    # 'linear' / 'cubic' griddata (Qhull Delaunay): not part of the accelerated path
     from scipy.interpolate import griddata
 
     out = griddata(points, values, (X, Y, Z), method=method, fill_value=0.0)

@@ -181,10 +181,46 @@ def rbf_cases(ref):
           kernel=np.array("thin_plate_spline"), k=20, smoothing=0.0, U=U, V=V, W=W)
 
 
+def nearest_cases(ref):
+    """method='nearest' (interpolator.py:196-197: griddata -> NearestNDInterpolator, a k=1
+    KDTree query).  Continuous draws: no two particles tie as a voxel's nearest."""
+    rng = np.random.default_rng(31)
+    P = rng.uniform(-0.5, 20.5, (3000, 3)); Q = rng.standard_normal((3000, 3))
+    x, y, z, U, V, W = _run(ref, P, Q, ((0, 21), (0, 18), (0, 15)), (21, 18, 15), method="nearest")
+    _save("nearest_small", points=P, values=Q, ax=x, ay=y, az=z, method=np.array("nearest"), k=1, power=2.0,
+          U=U, V=V, W=W)
+
+
+def div_cases(ref_path):
+    """physics.compute_consistent_divergence (physics.py:6-53), the divergence view_divergence.py:39
+    reads: float64 fields; float32 fields with Python-float spacings (float32 result) and with
+    numpy float64 spacings (float64 result, view_divergence.py:22-24); a one-plane axis; and the
+    masked sphere-pack IDW field of masked_case() with its grid spacing."""
+    sys.path.insert(0, ref_path)
+    import physics  # noqa: E402  (the reference module)
+
+    rng = np.random.default_rng(41)
+    shape = (20, 24, 28)
+    f = rng.standard_normal((3,) + shape)
+    m = rng.uniform(size=shape) < 0.7
+    cases = [("div_f64", f, m, (0.5, 1.25, 2.0)),
+             ("div_f32", f.astype(np.float32), m, (0.5, 1.25, 2.0)),
+             ("div_f32_np64", f.astype(np.float32), m, tuple(np.float64(h) for h in (0.75, 1.5, 0.3))),
+             ("div_flat", rng.standard_normal((3, 1, 5, 7)), rng.uniform(size=(1, 5, 7)) < 0.6, (1.0, 1.0, 1.0))]
+    g = np.load(os.path.join(HERE, "masked_spherepack_idw.npz"))
+    x = g["ax"]
+    h = x[1] - x[0]
+    cases.append(("div_masked_spherepack", np.stack([g["U"], g["V"], g["W"]]), g["mask"], (h, h, h)))
+    for name, F, M, (dx, dy, dz) in cases:
+        D = physics.compute_consistent_divergence(F[0], F[1], F[2], M, dx, dy, dz)
+        _save(name, u=F[0], v=F[1], w=F[2], mask=M, dx=np.float64(dx), dy=np.float64(dy), dz=np.float64(dz),
+              spacing_np64=int(isinstance(dx, np.floating)), div=D)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
-    ap.add_argument("--only", default="knn,edge,masked,rbf")
+    ap.add_argument("--only", default="knn,edge,masked,rbf,nearest,div")
     a = ap.parse_args()
     ref = _import_reference(a.ref)
     only = a.only.split(",")
@@ -196,6 +232,10 @@ def main():
         masked_case(ref)
     if "rbf" in only:
         rbf_cases(ref)
+    if "nearest" in only:
+        nearest_cases(ref)
+    if "div" in only:
+        div_cases(a.ref)
 
 
 if __name__ == "__main__":

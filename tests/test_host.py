@@ -58,9 +58,10 @@ def test_reference_exceptions_before_any_gpu_call(capsys):
 
 
 def test_griddata_methods_pass_through():
-    """linear/nearest stay scipy griddata (interpolator.py:196-197, outside the accelerated path)."""
+    """linear stays scipy griddata (interpolator.py:196-197, Qhull: outside the accelerated path);
+    nearest runs on the GPU k-NN kernel (tests/test_gpu_nearest_div.py)."""
     grid, _ = ip.create_grid(((0, 4),) * 3, 4)
-    U, V, W = ip.interpolate_field(_df(60), grid, method="nearest")
+    U, V, W = ip.interpolate_field(_df(60), grid, method="linear")
     assert U.shape == (4, 4, 4) and np.isfinite(U).all()
 
 
@@ -129,3 +130,20 @@ def test_rbf_argument_resolution_matches_scipy():
     assert it.neighbors == 30 and it.degree == 1 and it.epsilon == 1.0
     with pytest.raises(NotImplementedError):
         LocalRBFInterpolator(np.tile(P, (3, 1)), np.tile(D, (3, 1)), neighbors=61)  # 61 + 4 > 64
+
+
+def test_divergence_host_rules_before_any_gpu_call():
+    """physics mirror: the reference's exceptions and numpy's promotion, decided on the host."""
+    from ptv_interpolation_amd import physics
+
+    f = np.zeros((3, 4, 5))
+    with pytest.raises(np.exceptions.AxisError):
+        physics.compute_consistent_divergence(f, f, f, None, 1.0, 1.0, 1.0)
+    with pytest.raises(NotImplementedError):
+        physics.compute_consistent_divergence(f, f.astype(np.float32), f, f > 0, 1.0, 1.0, 1.0)
+    f32 = np.empty(0, np.float32).dtype
+    assert physics._result_dtype(f32, 0.5) == np.float32
+    assert physics._result_dtype(f32, np.float64(0.5)) == np.float64
+    assert physics._result_dtype(np.dtype(np.float64), np.float32(0.5)) == np.float64
+    x = np.linspace(0, 9, 10)
+    assert physics._result_dtype(f32, x[1] - x[0]) == np.float64  # view_divergence.py:22

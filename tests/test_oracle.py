@@ -99,3 +99,20 @@ def test_rbf_kernel_formulas_match_scipy(kernel):
     ref = _kernel_matrix(y, kernel)
     r = np.sqrt(((y[:, None, :] - y[None, :, :]) ** 2).sum(-1))
     assert np.allclose(cpu_ref.RBF_PHI[kernel](r), ref, rtol=1e-13, atol=1e-14)
+
+
+@pytest.mark.parametrize("name", names(("div_",)))
+def test_divergence_oracle_matches_reference(name):
+    """physics.compute_consistent_divergence golden vectors: bit-exact, same dtype."""
+    g = load(name)
+    sp = [g[k] if int(g["spacing_np64"]) else float(g[k]) for k in ("dx", "dy", "dz")]
+    d = cpu_ref.consistent_divergence(g["u"], g["v"], g["w"], g["mask"], *sp)
+    assert d.dtype == g["div"].dtype
+    assert np.array_equal(d, g["div"])
+
+
+def test_nearest_oracle_matches_reference():
+    g = load("nearest_small")
+    U, V, W = cpu_ref.interp_grid(g["points"], g["values"], g["ax"], g["ay"], g["az"], "nearest")
+    for a, b in ((U, g["U"]), (V, g["V"]), (W, g["W"])):
+        assert np.array_equal(a, b)
