@@ -79,6 +79,8 @@ struct DivArgs {
     int field_f32;           // fields are float32 (else float64)
     int result_f32;          // quotients and sums in float32 (else float64)
     double dx, dy, dz;
+    int ntx = 0, nty = 0, ntiles = 0;  // tile counts (set by the launcher)
+    int xcd = 0;                       // XCD-contiguous tile order
 };
 
 int launch_divergence(const DivArgs &a, const void *U, const void *V, const void *W, const uint8_t *M, void *out,
