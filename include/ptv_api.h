@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define PTV_API_VERSION 3
+#define PTV_API_VERSION 4
 
 /* error codes */
 #define PTV_OK 0
@@ -155,6 +155,49 @@ typedef struct {
     const uint8_t *fluid_mask;
 } ptv_div_params;
 
+/*
+ * Raw pore mask for sample_mask_on_grid (interpolator.py:205-238).  `raw` is
+ * (nz, ny, nx) C order, one byte per voxel, nonzero where the raw value
+ * `mask_raw.astype(float)` is > 0.5 (for a bool mask: the mask itself).  The axes are
+ * the raw voxel coordinates `linspace(min, max-1, n)` (or `[min]` when n == 1) and are
+ * always HOST arrays (n doubles each); `raw` lives in the call's memory space.
+ */
+typedef struct {
+    int64_t nx, ny, nz;
+    const uint8_t *raw;
+    const double *ax, *ay, *az;
+} ptv_mask_grid;
+
+/*
+ * Boundary particles (extract_boundary_particles, interpolator.py:240-284).
+ * mask: (nz, ny, nx) bytes.  encoding PTV_MASK_BOOL: bytes are 0/1 (a numpy bool mask);
+ * PTV_MASK_BITS: bit 1 = (value != 0), bit 0 = (value & 1) (an integer mask, for which
+ * numpy's `dilated & ~mask` keeps the low bit only).  Coordinates per axis (x, y, z):
+ * lo + (index * span) / den with span = max - 1 - min and den = n - 1
+ * (interpolator.py:278-280; the caller handles n == 1, where the reference returns ints).
+ */
+#define PTV_MASK_BOOL 0
+#define PTV_MASK_BITS 1
+typedef struct {
+    int64_t nx, ny, nz;
+    const uint8_t *mask;
+    int encoding;          /* PTV_MASK_BOOL | PTV_MASK_BITS */
+    int thickness;         /* binary_dilation iterations, >= 1 */
+    int64_t sampling_step; /* take every Nth boundary voxel (C order), >= 1 */
+    double lo[3], span[3], den[3];
+} ptv_boundary_params;
+
+/*
+ * k-NN median/MAD outlier filter (filtering.py:5-58 remove_outliers_knn).
+ * k: neighbours excluding the point itself (the reference queries k+1, :26), k <= 63;
+ * threshold: MAD units (:47-51); mad_eps: 1e-6 (:46).
+ */
+typedef struct {
+    int k;
+    double threshold;
+    double mad_eps;
+} ptv_filter_params;
+
 /* Library / device management. */
 int ptv_version(void);
 /* sizeof(ptv_particles, ptv_grid, ptv_knn_params, ptv_stats, ptv_rbf_params, ptv_div_params):
@@ -217,6 +260,48 @@ int ptv_divergence(ptv_ctx *ctx, const ptv_div_params *prm, const void *U, const
 /* Same on device pointers (fields, mask, out), enqueued on `stream` (NULL = ctx's). */
 int ptv_divergence_dev(ptv_ctx *ctx, const ptv_div_params *prm, const void *U, const void *V,
                        const void *W, void *out, void *stream, ptv_stats *st);
+
+/*
+ * Nearest-neighbour resampling of a raw mask onto the grid, host buffers.  Replaces
+ * sample_mask_on_grid (interpolator.py:205-238): RegularGridInterpolator((z, y, x),
+ * mask_raw.astype(float), method='nearest', bounds_error=False, fill_value=0) at every
+ * grid voxel, then `> 0.5`.  out: (z_end - z_begin, ny, nx) bytes, 1 = fluid.
+ */
+int ptv_sample_mask(ptv_ctx *ctx, const ptv_mask_grid *src, const ptv_grid *g, uint8_t *out);
+
+/* Same; src->raw, the grid arrays and `out` are DEVICE memory (src axes stay host). */
+int ptv_sample_mask_dev(ptv_ctx *ctx, const ptv_mask_grid *src, const ptv_grid *g, uint8_t *out,
+                        void *stream);
+
+/*
+ * Boundary particles, host buffers.  Replaces extract_boundary_particles
+ * (interpolator.py:240-284): binary_dilation(mask, 6-connected, iterations=thickness)
+ * & ~mask, np.where in C order, [::sampling_step], physical coordinates.
+ * *count receives the number of particles; x, y, z (cap entries each) are written only
+ * when cap >= *count (call once with cap = 0 to size them).
+ */
+int ptv_boundary_particles(ptv_ctx *ctx, const ptv_boundary_params *prm, double *x, double *y,
+                           double *z, int64_t cap, int64_t *count);
+
+/* Same; prm->mask and x, y, z are DEVICE memory.  Synchronises (the count is returned). */
+int ptv_boundary_particles_dev(ptv_ctx *ctx, const ptv_boundary_params *prm, double *x,
+                               double *y, double *z, int64_t cap, int64_t *count, void *stream);
+
+/*
+ * k-NN outlier filter, host buffers.  Replaces remove_outliers_knn (filtering.py:5-58):
+ * KDTree(points).query(points, k+1) minus the point itself (:20-30), the median and MAD
+ * of the neighbours' speeds (:38-44) and the z-score test (:47-51).
+ * keep: n bytes, 1 = keep (original particle order).  kth_dist: optional (NULL) n
+ * doubles, the distance to the (k+1)-th neighbour counting the point itself
+ * (`dist[:, -1]`, whose median the reference prints, :33-35).  Requires n > k
+ * (the reference skips the filter otherwise, :12-14).
+ */
+int ptv_filter_outliers_knn(ptv_ctx *ctx, const ptv_particles *p, const ptv_filter_params *prm,
+                            uint8_t *keep, double *kth_dist, ptv_stats *st);
+
+/* Same on device pointers, enqueued on `stream` (NULL = the ctx's own stream). */
+int ptv_filter_outliers_knn_dev(ptv_ctx *ctx, const ptv_particles *p, const ptv_filter_params *prm,
+                                uint8_t *keep, double *kth_dist, void *stream, ptv_stats *st);
 
 /*
  * Last-launch k-NN kernel duration in ms (hipEvent pair recorded around the

@@ -18,6 +18,12 @@ What it restates (reference = tombultreys/ptv_interpolation, read-only):
 * ``physics.compute_consistent_divergence`` (physics.py:6-53) as
   ``consistent_divergence`` below (an independent per-axis index restatement,
   not the reference's np.roll formulation)
+* ``interpolator.sample_mask_on_grid`` (interpolator.py:205-238, scipy
+  ``RegularGridInterpolator(method='nearest')`` restated as a per-axis interval
+  search) and ``interpolator.extract_boundary_particles`` (interpolator.py:240-284,
+  ``binary_dilation`` restated as padded face shifts) as ``sample_mask_nearest`` /
+  ``boundary_particles`` below
+* ``filtering.remove_outliers_knn`` (filtering.py:5-58) as ``outlier_filter``
 * the RBF process fan-out pattern (interpolator.py:173-182,
   test_parallel.py:6-28) as a z-slab ``ProcessPoolExecutor`` driver used as the
   same-box CPU baseline.
@@ -392,3 +398,99 @@ def consistent_divergence(u, v, w, mask, dx, dy, dz):
     vfn, vfp = _faces(np.asarray(v), fluid, 1)
     wfn, wfp = _faces(np.asarray(w), fluid, 0)
     return (ufn - ufp) / dx + (vfn - vfp) / dy + (wfn - wfp) / dz
+
+
+# ----------------------------------------------------------------------------
+# pore-mask path (interpolator.py:205-284) and the k-NN outlier filter (filtering.py:5-58)
+# ----------------------------------------------------------------------------
+def rgi_nearest_index(grid, x):
+    """RegularGridInterpolator 'nearest' index along one axis (scipy 1.15 _rgi.py
+    _find_indices / _evaluate_nearest / _find_out_of_bounds), -1 = out of bounds."""
+    g = np.asarray(grid, dtype=np.float64)
+    x = np.asarray(x, dtype=np.float64)
+    n = len(g)
+    flip = n > 1 and g[0] > g[-1]
+    if flip:
+        g = g[::-1]
+    oob = (x < g[0]) | (x > g[-1]) | np.isnan(x)
+    if n == 1:
+        j = np.zeros(x.shape, dtype=np.int64)
+    else:
+        i = np.clip(np.searchsorted(g, x, side="right") - 1, 0, n - 2)
+        t = (x - g[i]) / (g[i + 1] - g[i])
+        j = np.where(t <= 0.5, i, i + 1)
+    if flip:
+        j = n - 1 - j
+    return np.where(oob, -1, j)
+
+
+def sample_mask_nearest(mask_raw, bounds_raw, X, Y, Z):
+    """sample_mask_on_grid (interpolator.py:205-238): nearest raw voxel, 0 outside, > 0.5."""
+    raw = np.asarray(mask_raw).astype(float) > 0.5
+    nz, ny, nx = raw.shape
+    (xmin, xmax), (ymin, ymax), (zmin, zmax) = bounds_raw
+    axes = [np.linspace(lo, hi - 1, n) if n > 1 else np.array([lo], dtype=np.float64)
+            for lo, hi, n in ((zmin, zmax, nz), (ymin, ymax, ny), (xmin, xmax, nx))]
+    jz = rgi_nearest_index(axes[0], np.ravel(Z))
+    jy = rgi_nearest_index(axes[1], np.ravel(Y))
+    jx = rgi_nearest_index(axes[2], np.ravel(X))
+    ok = (jz >= 0) & (jy >= 0) & (jx >= 0)
+    out = np.zeros(jz.shape, dtype=bool)
+    out[ok] = raw[jz[ok], jy[ok], jx[ok]]
+    return out.reshape(np.shape(X))
+
+
+def _dilate6(a):
+    """One binary_dilation pass with the 6-connected cross and border_value 0."""
+    p = np.pad(a, 1, constant_values=False)
+    return (p[1:-1, 1:-1, 1:-1] | p[:-2, 1:-1, 1:-1] | p[2:, 1:-1, 1:-1] | p[1:-1, :-2, 1:-1]
+            | p[1:-1, 2:, 1:-1] | p[1:-1, 1:-1, :-2] | p[1:-1, 1:-1, 2:])
+
+
+def boundary_particles(mask, bounds, sampling_step=1, thickness=1):
+    """extract_boundary_particles (interpolator.py:240-284), dilation restated."""
+    if mask is None:
+        return np.array([]), np.array([]), np.array([])
+    m = np.asarray(mask)
+    nz, ny, nx = m.shape
+    (xmin, xmax), (ymin, ymax), (zmin, zmax) = bounds
+    g = m != 0
+    if thickness >= 1:
+        for _ in range(thickness):
+            g = _dilate6(g)
+    else:  # scipy: iterate until nothing changes
+        while True:
+            h = _dilate6(g)
+            if np.array_equal(h, g):
+                break
+            g = h
+    iz, iy, ix = np.nonzero(g & (~m))
+    if len(ix) == 0:
+        return np.array([]), np.array([]), np.array([])
+    if sampling_step > 1:
+        iz, iy, ix = iz[::sampling_step], iy[::sampling_step], ix[::sampling_step]
+
+    def phys(idx, lo, hi, n):
+        return lo + idx * (hi - 1 - lo) / (n - 1) if n > 1 else np.full_like(idx, lo)
+
+    return phys(ix, xmin, xmax, nx), phys(iy, ymin, ymax, ny), phys(iz, zmin, zmax, nz)
+
+
+def outlier_filter(points, values, k=25, threshold=3.0, workers=1):
+    """remove_outliers_knn (filtering.py:5-58) -> (keep mask, median k-th radius).
+
+    KDTree(points).query(points, k+1) with column 0 dropped, speed median and MAD over the
+    k neighbours, z = |speed - median| / (MAD + 1e-6) <= threshold."""
+    from scipy.spatial import KDTree
+
+    points = np.asarray(points, dtype=np.float64)
+    u, v, w = (np.asarray(values, dtype=np.float64)[:, c] for c in range(3))
+    speed = np.sqrt(u**2 + v**2 + w**2)
+    dist, idx = KDTree(points).query(points, k=k + 1, workers=workers)
+    nb = idx[:, 1:]
+    radius = np.median(dist[:, 1:][:, -1])
+    ns = speed[nb]
+    med = np.median(ns, axis=1)
+    mad = np.median(np.abs(ns - med[:, None]), axis=1)
+    z = np.abs(speed - med) / (mad + 1e-6)
+    return z <= threshold, radius

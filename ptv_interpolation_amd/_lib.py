@@ -78,6 +78,26 @@ class DivParams(C.Structure):
                 ("fluid_mask", C.POINTER(C.c_uint8))]
 
 
+_u8p = C.POINTER(C.c_uint8)
+MASK_BOOL = 0
+MASK_BITS = 1
+
+
+class MaskGrid(C.Structure):
+    _fields_ = [("nx", C.c_int64), ("ny", C.c_int64), ("nz", C.c_int64), ("raw", _u8p),
+                ("ax", _dp), ("ay", _dp), ("az", _dp)]
+
+
+class BoundaryParams(C.Structure):
+    _fields_ = [("nx", C.c_int64), ("ny", C.c_int64), ("nz", C.c_int64), ("mask", _u8p),
+                ("encoding", C.c_int), ("thickness", C.c_int), ("sampling_step", C.c_int64),
+                ("lo", C.c_double * 3), ("span", C.c_double * 3), ("den", C.c_double * 3)]
+
+
+class FilterParams(C.Structure):
+    _fields_ = [("k", C.c_int), ("threshold", C.c_double), ("mad_eps", C.c_double)]
+
+
 class Stats(C.Structure):
     _fields_ = [("ms_h2d", C.c_double), ("ms_bin", C.c_double), ("ms_lattice", C.c_double), ("ms_knn", C.c_double),
                 ("ms_d2h", C.c_double),
@@ -112,6 +132,16 @@ EXPORTS = {
                                  C.c_void_p, C.POINTER(Stats)]),
     "ptv_divergence_dev": (C.c_int, [C.c_void_p, C.POINTER(DivParams), C.c_void_p, C.c_void_p, C.c_void_p,
                                      C.c_void_p, C.c_void_p, C.POINTER(Stats)]),
+    "ptv_sample_mask": (C.c_int, [C.c_void_p, C.POINTER(MaskGrid), C.POINTER(Grid), _u8p]),
+    "ptv_sample_mask_dev": (C.c_int, [C.c_void_p, C.POINTER(MaskGrid), C.POINTER(Grid), _u8p, C.c_void_p]),
+    "ptv_boundary_particles": (C.c_int, [C.c_void_p, C.POINTER(BoundaryParams), _dp, _dp, _dp, C.c_int64,
+                                         C.POINTER(C.c_int64)]),
+    "ptv_boundary_particles_dev": (C.c_int, [C.c_void_p, C.POINTER(BoundaryParams), _dp, _dp, _dp, C.c_int64,
+                                             C.POINTER(C.c_int64), C.c_void_p]),
+    "ptv_filter_outliers_knn": (C.c_int, [C.c_void_p, C.POINTER(Particles), C.POINTER(FilterParams), _u8p, _dp,
+                                          C.POINTER(Stats)]),
+    "ptv_filter_outliers_knn_dev": (C.c_int, [C.c_void_p, C.POINTER(Particles), C.POINTER(FilterParams), _u8p,
+                                              _dp, C.c_void_p, C.POINTER(Stats)]),
     "ptv_last_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
     "ptv_debug_stamps": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_double)]),
 }
@@ -223,6 +253,62 @@ class Context:
                 "passes", "kept")
         v = list(out)
         return {"waves": v[0], "mean": dict(zip(keys, v[1:12])), "max": dict(zip(keys, v[12:23]))}
+
+    # -- pore-mask path and outlier filter -------
+    def sample_mask(self, raw, raw_axes, axes=None, grid_points=None, shape=None, z_range=None):
+        """Nearest resampling of a raw byte mask (1 = value > 0.5) onto a grid -> uint8 (nz', ny, nx).
+
+        raw: (rnz, rny, rnx) bytes; raw_axes: (x, y, z) raw voxel coordinates (host)."""
+        rw = np.ascontiguousarray(raw, dtype=np.uint8)
+        rnz, rny, rnx = rw.shape
+        rax, ray, raz = (np.ascontiguousarray(a, dtype=np.float64).ravel() for a in raw_axes)
+        M = MaskGrid(rnx, rny, rnz, rw.ctypes.data_as(_u8p), as_dp(rax), as_dp(ray), as_dp(raz))
+        keep = [rw, rax, ray, raz]
+        if axes is not None:
+            ax, ay, az = (np.ascontiguousarray(a, dtype=np.float64).ravel() for a in axes)
+            nx, ny, nz = len(ax), len(ay), len(az)
+            keep += [ax, ay, az]
+            G = Grid(nx, ny, nz, as_dp(ax), as_dp(ay), as_dp(az), None, None, None, 0, nz)
+        else:
+            nz, ny, nx = shape
+            gp = [np.ascontiguousarray(a, dtype=np.float64).ravel() for a in grid_points]
+            keep += gp
+            G = Grid(nx, ny, nz, None, None, None, as_dp(gp[0]), as_dp(gp[1]), as_dp(gp[2]), 0, nz)
+        z0, z1 = (0, nz) if z_range is None else z_range
+        G.z_begin, G.z_end = z0, z1
+        out = np.empty((z1 - z0, ny, nx), dtype=np.uint8)
+        check(lib().ptv_sample_mask(self.h, C.byref(M), C.byref(G), out.ctypes.data_as(_u8p)))
+        return out
+
+    def boundary_particles(self, mask_bytes, encoding, thickness, step, lo, span, den):
+        """Boundary voxel coordinates (x, y, z) float64 arrays; mask_bytes (nz, ny, nx) uint8."""
+        mb = np.ascontiguousarray(mask_bytes, dtype=np.uint8)
+        nz, ny, nx = mb.shape
+        prm = BoundaryParams(nx, ny, nz, mb.ctypes.data_as(_u8p), int(encoding), int(thickness), int(step),
+                             (C.c_double * 3)(*lo), (C.c_double * 3)(*span), (C.c_double * 3)(*den))
+        cnt = C.c_int64(0)
+        check(lib().ptv_boundary_particles(self.h, C.byref(prm), None, None, None, 0, C.byref(cnt)))
+        n = cnt.value
+        out = [np.empty(n, dtype=np.float64) for _ in range(3)]
+        if n > 0:
+            check(lib().ptv_boundary_particles(self.h, C.byref(prm), as_dp(out[0]), as_dp(out[1]),
+                                               as_dp(out[2]), n, C.byref(cnt)))
+        return tuple(out)
+
+    def filter_outliers_knn(self, points, values, k=25, threshold=3.0, mad_eps=1e-6):
+        """(keep uint8 (n,), kth_dist float64 (n,)) of the median/MAD k-NN filter."""
+        pts = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 3)
+        vals = np.ascontiguousarray(values, dtype=np.float64).reshape(-1, 3)
+        cols = [np.ascontiguousarray(pts[:, i]) for i in range(3)] + [np.ascontiguousarray(vals[:, i]) for i in range(3)]
+        P = Particles(pts.shape[0], *[as_dp(c) for c in cols])
+        prm = FilterParams(int(k), float(threshold), float(mad_eps))
+        keep = np.empty(pts.shape[0], dtype=np.uint8)
+        kth = np.empty(pts.shape[0], dtype=np.float64)
+        st = Stats()
+        check(lib().ptv_filter_outliers_knn(self.h, C.byref(P), C.byref(prm), keep.ctypes.data_as(_u8p),
+                                            as_dp(kth), C.byref(st)))
+        self.stats = st.as_dict()
+        return keep, kth
 
     # -- host buffers ------------------------------------------------------
     def interp_knn(self, points, values, axes=None, grid_points=None, shape=None, method=METHOD_IDW, k=8,

@@ -72,6 +72,14 @@ struct ptv_ctx {
     DevBuf<int> rbf_pw, rbf_status;                              // monomial exponents, singular count
     DevBuf<double> smooth;                                       // per-particle smoothing (host calls)
     DevBuf<uint8_t> fld[4];                                      // divergence host calls: U, V, W, out
+    DevBuf<double> mask_axes;                                    // sample_mask: raw axes (ascending)
+    DevBuf<int> mask_tabs;                                       // sample_mask: per-axis index tables
+    DevBuf<uint8_t> mask_raw, mask_out;                          // sample_mask host calls
+    DevBuf<uint8_t> bnd_ping, bnd_pong;                          // boundary: dilation passes
+    DevBuf<unsigned long long> bnd_counts;                       // boundary: per-block counts / offsets
+    DevBuf<double> bnd_xyz;                                      // boundary host calls: coordinates
+    DevBuf<uint8_t> flt_keep;                                    // outlier filter host calls
+    DevBuf<double> flt_kth;
     hipEvent_t ev_div0 = nullptr, ev_div1 = nullptr;             // around the divergence stencil
     bool div_pending = false;
     std::vector<hipEvent_t> rbf_ev;                              // 3 per chunk: knn start, solve start, end
@@ -174,6 +182,16 @@ int ptv_free(ptv_ctx *c) {
     c->rbf_status.release();
     c->smooth.release();
     for (auto &b : c->fld) b.release();
+    c->mask_axes.release();
+    c->mask_tabs.release();
+    c->mask_raw.release();
+    c->mask_out.release();
+    c->bnd_ping.release();
+    c->bnd_pong.release();
+    c->bnd_counts.release();
+    c->bnd_xyz.release();
+    c->flt_keep.release();
+    c->flt_kth.release();
     hipEventDestroy(c->ev_div0);
     hipEventDestroy(c->ev_div1);
     for (hipEvent_t e : c->rbf_ev) hipEventDestroy(e);
@@ -999,6 +1017,332 @@ int ptv_last_stats(ptv_ctx *c, ptv_stats *st) {
     PTV_HIP(hipSetDevice(c->device));
     PTV_TRY(finish_timing(c));
     *st = c->last;
+    return PTV_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// pore-mask path and outlier filter
+// ---------------------------------------------------------------------------
+namespace {
+
+// raw axes -> device (ascending; a descending axis is reversed and flagged, as scipy's
+// RegularGridInterpolator flips descending grids, _rgi.py _check_dimensionality/flip)
+int mask_source(ptv_ctx *c, const ptv_mask_grid *src, MaskSampleLaunch &m, hipStream_t s) {
+    if (!src || !src->raw || !src->ax || !src->ay || !src->az) {
+        set_error("sample_mask: NULL raw mask or axis");
+        return PTV_E_ARG;
+    }
+    const int64_t rn[3] = {src->nx, src->ny, src->nz};
+    for (int d = 0; d < 3; ++d)
+        if (rn[d] <= 0 || rn[d] > (1 << 30)) {
+            set_error("sample_mask: raw mask extents must be positive");
+            return PTV_E_ARG;
+        }
+    std::vector<double> h;
+    h.reserve(rn[0] + rn[1] + rn[2]);
+    const double *ax[3] = {src->ax, src->ay, src->az};
+    size_t off[3];
+    for (int d = 0; d < 3; ++d) {
+        const double *a = ax[d];
+        const int64_t n = rn[d];
+        const bool desc = n > 1 && a[0] > a[n - 1];
+        off[d] = h.size();
+        for (int64_t i = 0; i < n; ++i) h.push_back(desc ? a[n - 1 - i] : a[i]);
+        for (int64_t i = 1; i < n; ++i)
+            if (!(h[off[d] + i] > h[off[d] + i - 1])) {
+                set_error("The points in dimension " + std::to_string(2 - d) +
+                          " must be strictly ascending or descending");
+                return PTV_E_ARG;
+            }
+        m.rn[d] = (int)n;
+        m.flip[d] = desc ? 1 : 0;
+    }
+    PTV_TRY(c->mask_axes.ensure(h.size()));
+    PTV_HIP(hipMemcpyAsync(c->mask_axes.p, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice, s));
+    for (int d = 0; d < 3; ++d) m.ra[d] = c->mask_axes.p + off[d];
+    // the host vector must outlive the async copy
+    PTV_HIP(hipStreamSynchronize(s));
+    return PTV_OK;
+}
+
+int mask_grid_check(const ptv_grid *g, uint8_t *out) {
+    if (!g || !out) {
+        set_error("sample_mask: NULL grid or output");
+        return PTV_E_ARG;
+    }
+    if (g->nx <= 0 || g->ny <= 0 || g->nz <= 0 || g->nx > (1 << 30) || g->ny > (1 << 30) || g->nz > (1 << 30)) {
+        set_error("grid: dimensions must be positive");
+        return PTV_E_ARG;
+    }
+    const bool sep = g->ax && g->ay && g->az, pts = g->px && g->py && g->pz;
+    if (!sep && !pts) {
+        set_error("grid: give either the three axes or the three point arrays");
+        return PTV_E_ARG;
+    }
+    if (g->z_begin < 0 || g->z_end > g->nz || g->z_begin > g->z_end) {
+        set_error("grid: bad z slab");
+        return PTV_E_ARG;
+    }
+    return PTV_OK;
+}
+
+int run_mask_sample(ptv_ctx *c, MaskSampleLaunch &m, const ptv_grid *g, const uint8_t *raw, uint8_t *out,
+                    hipStream_t s) {
+    const bool sep = g->ax && g->ay && g->az;
+    m.raw = raw;
+    m.nx = (int)g->nx;
+    m.ny = (int)g->ny;
+    m.nz = (int)g->nz;
+    m.z0 = (int)g->z_begin;
+    m.z1 = (int)g->z_end;
+    PTV_TRY(c->mask_tabs.ensure(g->nx + g->ny + g->nz));
+    return launch_mask_sample(m, sep ? g->ax : nullptr, sep ? g->ay : nullptr, sep ? g->az : nullptr,
+                              sep ? nullptr : g->px, sep ? nullptr : g->py, sep ? nullptr : g->pz, c->mask_tabs.p,
+                              out, s);
+}
+
+int boundary_check(ptv_ctx *c, const ptv_boundary_params *prm, int64_t *count, BoundaryLaunch &m) {
+    if (!c || !prm || !prm->mask || !count) {
+        set_error("boundary: NULL context, params, mask or count");
+        return PTV_E_ARG;
+    }
+    if (prm->nx <= 0 || prm->ny <= 0 || prm->nz <= 0 || prm->nx > (1 << 30) || prm->ny > (1 << 30) ||
+        prm->nz > (1 << 30)) {
+        set_error("boundary: dimensions must be positive");
+        return PTV_E_ARG;
+    }
+    if (prm->thickness < 1 || prm->sampling_step < 1 ||
+        (prm->encoding != PTV_MASK_BOOL && prm->encoding != PTV_MASK_BITS)) {
+        set_error("boundary: need thickness >= 1, sampling_step >= 1 and a known encoding");
+        return PTV_E_ARG;
+    }
+    m.nx = (int)prm->nx;
+    m.ny = (int)prm->ny;
+    m.nz = (int)prm->nz;
+    m.mask = prm->mask;
+    m.is_bool = prm->encoding == PTV_MASK_BOOL;
+    m.thickness = prm->thickness;
+    m.step = prm->sampling_step;
+    for (int d = 0; d < 3; ++d) {
+        m.lo[d] = prm->lo[d];
+        m.span[d] = prm->span[d];
+        m.den[d] = prm->den[d];
+    }
+    PTV_HIP(hipSetDevice(c->device));
+    return PTV_OK;
+}
+
+// count pass (dilations + block counts + scan), then the emit pass into x, y, z if they fit
+int run_boundary(ptv_ctx *c, const BoundaryLaunch &m, double *x, double *y, double *z, int64_t cap, int64_t *count,
+                 hipStream_t s) {
+    const int64_t nvox = (int64_t)m.nx * m.ny * m.nz;
+    const size_t nb = boundary_blocks(nvox);
+    PTV_TRY(c->bnd_counts.ensure(nb + 1));
+    if (m.thickness > 1) {
+        PTV_TRY(c->bnd_ping.ensure(nvox));
+        if (m.thickness > 2) PTV_TRY(c->bnd_pong.ensure(nvox));
+    }
+    const uint8_t *grown = nullptr;
+    PTV_HIP(hipEventRecord(c->ev_div0, s));
+    PTV_TRY(launch_boundary_count(m, c->bnd_ping.p, c->bnd_pong.p, c->bnd_counts.p, &grown, s));
+    unsigned long long total = 0;
+    PTV_HIP(hipMemcpyAsync(&total, c->bnd_counts.p + nb, sizeof(total), hipMemcpyDeviceToHost, s));
+    PTV_HIP(hipStreamSynchronize(s));
+    const int64_t nsel = (int64_t)((total + (unsigned long long)m.step - 1) / (unsigned long long)m.step);
+    *count = nsel;
+    if (x && y && z && cap >= nsel && nsel > 0)
+        PTV_TRY(launch_boundary_emit(m, grown, c->bnd_counts.p, x, y, z, s));
+    PTV_HIP(hipEventRecord(c->ev_div1, s));
+    c->div_pending = true;
+    return PTV_OK;
+}
+
+int filter_check(ptv_ctx *c, const ptv_particles *p, const ptv_filter_params *prm, uint8_t *keep) {
+    if (!c || !p || !prm || !keep) {
+        set_error("filter: NULL context, particles, params or keep");
+        return PTV_E_ARG;
+    }
+    if (p->n <= 0 || !p->x || !p->y || !p->z || !p->u || !p->v || !p->w) {
+        set_error("particles: need n > 0 and six non-NULL arrays");
+        return PTV_E_ARG;
+    }
+    if (p->n >= (int64_t)1 << 31) {
+        set_error("particles: n must be < 2^31");
+        return PTV_E_ARG;
+    }
+    if (prm->k < 1 || filter_kmax(prm->k) == 0) {
+        set_error("filter: k must be in [1, 63]");
+        return PTV_E_UNSUPPORTED;
+    }
+    if (p->n <= prm->k) {
+        set_error("filter: need more particles than k (the reference skips the filter)");
+        return PTV_E_ARG;
+    }
+    PTV_HIP(hipSetDevice(c->device));
+    return PTV_OK;
+}
+
+// (k+1)-NN of every particle among the particles (slot mode, binned query order), then
+// the per-particle median / MAD statistics
+int run_filter(ptv_ctx *c, const ptv_particles *p, const ptv_filter_params *prm, uint8_t *keep, double *kth,
+               hipStream_t s) {
+    const int64_t n = p->n;
+    const int64_t npad = (n + 63) & ~(int64_t)63;  // 64 queries per wave tile (4 x 4 x 4)
+    for (int i = 0; i < 3; ++i) PTV_TRY(c->qpts[i].ensure(npad));
+    PTV_TRY(launch_pad_queries(p->x, p->y, p->z, n, npad, c->qpts[0].p, c->qpts[1].p, c->qpts[2].p, s));
+    ptv_grid g{};
+    g.nx = 4;
+    g.ny = 4;
+    g.nz = npad / 16;
+    g.px = c->qpts[0].p;
+    g.py = c->qpts[1].p;
+    g.pz = c->qpts[2].p;
+    g.z_begin = 0;
+    g.z_end = g.nz;
+    const SearchParams sp{PTV_METHOD_IDW, prm->k + 1, 2.0, 1e-10, 0u, 0.0, 0.0, -1};
+    KnnLaunch kl;
+    Binned b{};
+    PTV_TRY(prepare(c, p, &g, &sp, nullptr, nullptr, nullptr, g.px, g.py, g.pz, s, kl, b));
+    // the binned order as the query order: a wave's 64 queries are 64 neighbouring records
+    PTV_TRY(launch_binned_queries(b.prec, n, npad, c->qpts[0].p, c->qpts[1].p, c->qpts[2].p, s));
+    PTV_TRY(c->slots.ensure((size_t)npad * (prm->k + 1)));
+    kl.mode = kModeSlots;
+    kl.slots = c->slots.p;
+    c->rbf_chunks = 0;
+    PTV_TRY(launch_knn(kl, b, nullptr, nullptr, nullptr, c->qpts[0].p, c->qpts[1].p, c->qpts[2].p, nullptr, nullptr,
+                       nullptr, nullptr, s));
+    FilterArgs fa{n, prm->k, prm->threshold, prm->mad_eps};
+    PTV_TRY(launch_outlier_stats(fa, b, c->slots.p, keep, kth, s));
+    PTV_HIP(hipEventRecord(c->ev_knn1, s));
+    c->timed_pending = true;
+    c->last.n_voxels = n;
+    return PTV_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ptv_sample_mask_dev(ptv_ctx *c, const ptv_mask_grid *src, const ptv_grid *g, uint8_t *out, void *stream) {
+    if (!c) {
+        set_error("NULL context");
+        return PTV_E_ARG;
+    }
+    PTV_TRY(mask_grid_check(g, out));
+    PTV_HIP(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    MaskSampleLaunch m{};
+    PTV_TRY(mask_source(c, src, m, s));
+    return run_mask_sample(c, m, g, src->raw, out, s);
+}
+
+int ptv_sample_mask(ptv_ctx *c, const ptv_mask_grid *src, const ptv_grid *g, uint8_t *out) {
+    if (!c) {
+        set_error("NULL context");
+        return PTV_E_ARG;
+    }
+    PTV_TRY(mask_grid_check(g, out));
+    PTV_HIP(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    MaskSampleLaunch m{};
+    PTV_TRY(mask_source(c, src, m, s));
+    const int64_t nraw = src->nx * src->ny * src->nz;
+    PTV_TRY(c->mask_raw.ensure(nraw));
+    PTV_HIP(hipMemcpyAsync(c->mask_raw.p, src->raw, nraw, hipMemcpyHostToDevice, s));
+    ptv_grid dg = *g;
+    const int64_t plane = g->nx * g->ny, nfull = g->nz * plane, nout = (g->z_end - g->z_begin) * plane;
+    if (g->ax && g->ay && g->az) {
+        PTV_TRY(c->axes.ensure(g->nx + g->ny + g->nz));
+        PTV_HIP(hipMemcpyAsync(c->axes.p, g->ax, g->nx * sizeof(double), hipMemcpyHostToDevice, s));
+        PTV_HIP(hipMemcpyAsync(c->axes.p + g->nx, g->ay, g->ny * sizeof(double), hipMemcpyHostToDevice, s));
+        PTV_HIP(hipMemcpyAsync(c->axes.p + g->nx + g->ny, g->az, g->nz * sizeof(double), hipMemcpyHostToDevice, s));
+        dg.ax = c->axes.p;
+        dg.ay = c->axes.p + g->nx;
+        dg.az = c->axes.p + g->nx + g->ny;
+        dg.px = dg.py = dg.pz = nullptr;
+    } else {
+        const double *q[3] = {g->px, g->py, g->pz};
+        for (int i = 0; i < 3; ++i) {
+            PTV_TRY(c->qpts[i].ensure(nfull));
+            PTV_HIP(hipMemcpyAsync(c->qpts[i].p, q[i], nfull * sizeof(double), hipMemcpyHostToDevice, s));
+        }
+        dg.ax = dg.ay = dg.az = nullptr;
+        dg.px = c->qpts[0].p;
+        dg.py = c->qpts[1].p;
+        dg.pz = c->qpts[2].p;
+    }
+    PTV_TRY(c->mask_out.ensure(nout));
+    PTV_TRY(run_mask_sample(c, m, &dg, c->mask_raw.p, c->mask_out.p, s));
+    PTV_HIP(hipMemcpyAsync(out, c->mask_out.p, nout, hipMemcpyDeviceToHost, s));
+    PTV_HIP(hipStreamSynchronize(s));
+    return PTV_OK;
+}
+
+int ptv_boundary_particles_dev(ptv_ctx *c, const ptv_boundary_params *prm, double *x, double *y, double *z,
+                               int64_t cap, int64_t *count, void *stream) {
+    BoundaryLaunch m{};
+    PTV_TRY(boundary_check(c, prm, count, m));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    PTV_TRY(run_boundary(c, m, x, y, z, cap, count, s));
+    PTV_HIP(hipStreamSynchronize(s));
+    return PTV_OK;
+}
+
+int ptv_boundary_particles(ptv_ctx *c, const ptv_boundary_params *prm, double *x, double *y, double *z, int64_t cap,
+                           int64_t *count) {
+    BoundaryLaunch m{};
+    PTV_TRY(boundary_check(c, prm, count, m));
+    hipStream_t s = c->stream;
+    const int64_t nvox = prm->nx * prm->ny * prm->nz;
+    PTV_TRY(c->mask_raw.ensure(nvox));
+    PTV_HIP(hipMemcpyAsync(c->mask_raw.p, prm->mask, nvox, hipMemcpyHostToDevice, s));
+    m.mask = c->mask_raw.p;
+    // size the device output from the count pass when the caller's buffers are large enough
+    int64_t nsel = 0;
+    PTV_TRY(run_boundary(c, m, nullptr, nullptr, nullptr, 0, &nsel, s));
+    *count = nsel;
+    if (x && y && z && cap >= nsel && nsel > 0) {
+        PTV_TRY(c->bnd_xyz.ensure((size_t)3 * nsel));
+        double *d = c->bnd_xyz.p;
+        PTV_TRY(run_boundary(c, m, d, d + nsel, d + 2 * nsel, nsel, &nsel, s));
+        PTV_HIP(hipMemcpyAsync(x, d, nsel * sizeof(double), hipMemcpyDeviceToHost, s));
+        PTV_HIP(hipMemcpyAsync(y, d + nsel, nsel * sizeof(double), hipMemcpyDeviceToHost, s));
+        PTV_HIP(hipMemcpyAsync(z, d + 2 * nsel, nsel * sizeof(double), hipMemcpyDeviceToHost, s));
+    }
+    PTV_HIP(hipStreamSynchronize(s));
+    return PTV_OK;
+}
+
+int ptv_filter_outliers_knn_dev(ptv_ctx *c, const ptv_particles *p, const ptv_filter_params *prm, uint8_t *keep,
+                                double *kth_dist, void *stream, ptv_stats *st) {
+    PTV_TRY(filter_check(c, p, prm, keep));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    PTV_TRY(run_filter(c, p, prm, keep, kth_dist, s));
+    if (st) *st = c->last;
+    return PTV_OK;
+}
+
+int ptv_filter_outliers_knn(ptv_ctx *c, const ptv_particles *p, const ptv_filter_params *prm, uint8_t *keep,
+                            double *kth_dist, ptv_stats *st) {
+    PTV_TRY(filter_check(c, p, prm, keep));
+    hipStream_t s = c->stream;
+    const int64_t n = p->n;
+    const double *src[6] = {p->x, p->y, p->z, p->u, p->v, p->w};
+    for (int i = 0; i < 6; ++i) {
+        PTV_TRY(c->pin[i].ensure(n));
+        PTV_HIP(hipMemcpyAsync(c->pin[i].p, src[i], n * sizeof(double), hipMemcpyHostToDevice, s));
+    }
+    ptv_particles dp{n, c->pin[0].p, c->pin[1].p, c->pin[2].p, c->pin[3].p, c->pin[4].p, c->pin[5].p};
+    PTV_TRY(c->flt_keep.ensure(n));
+    PTV_TRY(c->flt_kth.ensure(n));
+    PTV_TRY(run_filter(c, &dp, prm, c->flt_keep.p, c->flt_kth.p, s));
+    PTV_HIP(hipMemcpyAsync(keep, c->flt_keep.p, n, hipMemcpyDeviceToHost, s));
+    if (kth_dist) PTV_HIP(hipMemcpyAsync(kth_dist, c->flt_kth.p, n * sizeof(double), hipMemcpyDeviceToHost, s));
+    PTV_HIP(hipStreamSynchronize(s));
+    PTV_TRY(finish_timing(c));
+    if (st) *st = c->last;
     return PTV_OK;
 }
 

@@ -110,4 +110,49 @@ int launch_rbf(const RbfKernelArgs &ka, const Binned &b, const uint32_t *slots, 
                const double *az, const double *qx, const double *qy, const double *qz, const double *smooth,
                const int *pw, const uint8_t *mask, double *U, double *V, double *W, int *status, hipStream_t s);
 
+// ---- pore-mask path (ptv_mask.hip) ----
+struct MaskSampleLaunch {
+    int rn[3];             // raw mask extents x, y, z
+    int flip[3];           // caller axis is descending (ra[d] holds it reversed)
+    const double *ra[3];   // raw mask axes, ascending (device)
+    const uint8_t *raw;    // (rn[2], rn[1], rn[0]) bytes, 1 = raw value > 0.5
+    int nx, ny, nz;        // grid
+    int z0, z1;            // planes sampled
+};
+// tabs: nx + ny + nz ints of scratch (separable grids)
+int launch_mask_sample(const MaskSampleLaunch &m, const double *ax, const double *ay, const double *az,
+                       const double *px, const double *py, const double *pz, int *tabs, uint8_t *out,
+                       hipStream_t s);
+
+struct BoundaryLaunch {
+    int nx, ny, nz;
+    const uint8_t *mask;   // (nz, ny, nx); bool bytes, or bit1 = nonzero | bit0 = low bit
+    int is_bool;
+    int thickness;         // >= 1 dilation iterations
+    int64_t step;          // sampling_step >= 1
+    double lo[3], span[3], den[3];  // x, y, z: lo + (idx * span) / den
+};
+size_t boundary_blocks(int64_t nvox);
+// dilation passes + per-block counts + their exclusive scan (counts: boundary_blocks + 1
+// entries, total at [nb]); ping/pong: nvox bytes each when thickness > 1
+int launch_boundary_count(const BoundaryLaunch &m, uint8_t *ping, uint8_t *pong, unsigned long long *counts,
+                          const uint8_t **grown_out, hipStream_t s);
+int launch_boundary_emit(const BoundaryLaunch &m, const uint8_t *grown, const unsigned long long *offsets,
+                         double *ox, double *oy, double *oz, hipStream_t s);
+
+// ---- k-NN outlier filter (ptv_filter.hip) ----
+struct FilterArgs {
+    int64_t n;
+    int k;               // neighbours without the point itself
+    double threshold;
+    double mad_eps;
+};
+int filter_kmax(int k);
+int launch_pad_queries(const double *x, const double *y, const double *z, int64_t n, int64_t npad, double *qx,
+                       double *qy, double *qz, hipStream_t s);
+int launch_binned_queries(const double4 *prec, int64_t n, int64_t npad, double *qx, double *qy, double *qz,
+                          hipStream_t s);
+int launch_outlier_stats(const FilterArgs &a, const Binned &b, const uint32_t *slots, uint8_t *keep, double *kth,
+                         hipStream_t s);
+
 }  // namespace ptv

@@ -96,41 +96,74 @@ def create_grid(bounds, resolution, dense=True):
 
 
 def sample_mask_on_grid(mask_raw, grid_tuple, bounds_raw):
-    """Nearest-neighbour resampling of a raw mask onto the grid; interpolator.py:205-238."""
-    from scipy.interpolate import RegularGridInterpolator
+    """Nearest-neighbour resampling of a raw mask onto the grid; interpolator.py:205-238.
 
-    nz, ny, nx = mask_raw.shape
+    The reference builds ``RegularGridInterpolator((z, y, x), mask_raw.astype(float),
+    method='nearest', bounds_error=False, fill_value=0)`` over the raw axes
+    ``linspace(min, max-1, n)`` and thresholds the samples at 0.5.  Here the raw mask goes
+    to the GPU as bytes (1 = value > 0.5; a bool mask as is) and ``ptv_sample_mask`` does
+    the per-voxel nearest lookup (scipy's interval search + ``t <= 0.5`` rule, out of
+    bounds -> 0) and the gather (ptv_interpolation_amd/csrc/ptv_mask.hip).
+    """
+    raw = np.asarray(mask_raw)
+    nz, ny, nx = raw.shape
     (xmin, xmax), (ymin, ymax), (zmin, zmax) = bounds_raw
     X, Y, Z = grid_tuple
     axes = []
-    for lo, hi, n in ((zmin, zmax, nz), (ymin, ymax, ny), (xmin, xmax, nx)):
-        axes.append(np.linspace(lo, hi - 1, n) if n > 1 else np.array([lo]))
-    rgi = RegularGridInterpolator(tuple(axes), mask_raw.astype(float), method="nearest",
-                                  bounds_error=False, fill_value=0)
-    pts = np.stack([np.ravel(Z), np.ravel(Y), np.ravel(X)], axis=-1)
-    return rgi(pts).reshape(X.shape) > 0.5
+    for lo, hi, n in ((xmin, xmax, nx), (ymin, ymax, ny), (zmin, zmax, nz)):
+        axes.append(np.linspace(lo, hi - 1, n) if n > 1 else np.array([lo], dtype=np.float64))
+    if raw.dtype == np.bool_:
+        raw_bytes = raw.view(np.uint8)
+    else:
+        raw_bytes = (raw.astype(float) > 0.5).view(np.uint8)
+    ctx = _lib.Context.get(_gpu_device())
+    sep = separable_axes(X, Y, Z)
+    shape = np.shape(X)
+    if sep is not None:
+        out = ctx.sample_mask(raw_bytes, axes, axes=sep)
+    else:
+        n = int(np.size(X))
+        out = ctx.sample_mask(raw_bytes, axes, grid_points=(np.ravel(X), np.ravel(Y), np.ravel(Z)),
+                              shape=(1, 1, n))
+    return out.view(np.bool_).reshape(shape)
 
 
 def extract_boundary_particles(mask, bounds, sampling_step=1, thickness=1):
-    """Solid voxels within `thickness` 6-connected steps of fluid -> coordinates; interpolator.py:240-284."""
-    import scipy.ndimage
+    """Solid voxels within `thickness` 6-connected steps of fluid -> coordinates; interpolator.py:240-284.
 
+    ``binary_dilation(mask, generate_binary_structure(3, 1), iterations=thickness) & ~mask``,
+    ``np.where`` (C order), ``[::sampling_step]`` and ``lo + idx * (hi - 1 - lo) / (n - 1)``
+    run on the GPU (``ptv_boundary_particles``: dilation passes, a fused last pass with a
+    per-block count, a scan, and an ordered emit).
+    """
     if mask is None:
         return np.array([]), np.array([]), np.array([])
-    nz, ny, nx = mask.shape
+    m = np.asarray(mask)
+    nz, ny, nx = m.shape
     (xmin, xmax), (ymin, ymax), (zmin, zmax) = bounds
-    st = scipy.ndimage.generate_binary_structure(3, 1)
-    grown = scipy.ndimage.binary_dilation(mask, structure=st, iterations=thickness)
-    iz, iy, ix = np.where(grown & ~mask)
-    if len(ix) == 0:
+    if m.dtype == np.bool_:
+        mb, enc = m.view(np.uint8), _lib.MASK_BOOL
+    else:
+        _ = ~m.reshape(-1)[:1]  # the reference's `~mask` (TypeError for float masks)
+        mb = ((m != 0).astype(np.uint8) << 1) | (m & 1).astype(np.uint8)
+        enc = _lib.MASK_BITS
+    # scipy: iterations < 1 repeats the dilation until nothing changes; nx + ny + nz
+    # passes reach every voxel of the box
+    t = int(thickness) if thickness >= 1 else nx + ny + nz
+    step = int(sampling_step) if sampling_step > 1 else 1
+    lo = (xmin, ymin, zmin)
+    span = (xmax - 1 - xmin, ymax - 1 - ymin, zmax - 1 - zmin)
+    ns = (nx, ny, nz)
+    den = tuple(float(n - 1) if n > 1 else 1.0 for n in ns)
+    ctx = _lib.Context.get(_gpu_device())
+    coords = ctx.boundary_particles(mb, enc, t, step, [float(v) for v in lo], [float(v) for v in span], den)
+    if len(coords[0]) == 0:
         return np.array([]), np.array([]), np.array([])
-    if sampling_step > 1:
-        iz, iy, ix = iz[::sampling_step], iy[::sampling_step], ix[::sampling_step]
-
-    def phys(idx, lo, hi, n):
-        return lo + idx * (hi - 1 - lo) / (n - 1) if n > 1 else np.full_like(idx, lo)
-
-    return phys(ix, xmin, xmax, nx), phys(iy, ymin, ymax, ny), phys(iz, zmin, zmax, nz)
+    out = []
+    for c, n, l in zip(coords, ns, lo):
+        # n == 1: np.full_like(int64 indices, min) in the reference
+        out.append(c if n > 1 else np.full_like(np.empty(len(c), dtype=np.int64), l))
+    return tuple(out)
 
 
 # ---------------------------------------------------------------------------

@@ -217,10 +217,91 @@ def div_cases(ref_path):
               spacing_np64=int(isinstance(dx, np.floating)), div=D)
 
 
+def _blob_mask(shape, n_spheres, seed):
+    """Random union of solid spheres (False) in fluid (True), any shape."""
+    rng = np.random.default_rng(seed)
+    nz, ny, nx = shape
+    Z, Y, X = np.meshgrid(np.arange(nz), np.arange(ny), np.arange(nx), indexing="ij")
+    fluid = np.ones(shape, dtype=bool)
+    for _ in range(n_spheres):
+        c = rng.uniform(0, 1, 3) * np.array([nx, ny, nz])
+        r = rng.uniform(2.0, 0.25 * min(shape) + 2.0)
+        fluid &= (X - c[0]) ** 2 + (Y - c[1]) ** 2 + (Z - c[2]) ** 2 > r * r
+    return fluid
+
+
+def mask_cases(ref):
+    """Pore-mask path: sample_mask_on_grid (interpolator.py:205-238) and
+    extract_boundary_particles (interpolator.py:240-284) on bool, non-cubic and integer masks."""
+    sys.path.insert(0, os.path.join(HERE, "..", ".."))
+    from ptv_interpolation_amd import synth
+
+    sphere = synth.fluid_mask(48)
+    blob = _blob_mask((20, 27, 33), 9, 5)
+    labels = np.random.default_rng(6).integers(0, 4, (14, 17, 19)).astype(np.uint8)
+    labels[:, :, :6] = 0
+    raws = {"sphere48": (sphere, ((0, 48),) * 3), "blob": (blob, ((0, 33), (0, 27), (0, 20))),
+            "blob_off": (blob, ((2.5, 40.25), (-3.0, 30.0), (10, 30)))}
+    # (raw, grid bounds, grid resolution (nx, ny, nz)); wider grid bounds put voxels out of bounds,
+    # 95 points on [0, 47] put grid points exactly half way between raw voxels (t = 0.5 ties)
+    samples = [("sphere48", ((0, 48),) * 3, (32, 32, 32)),
+               ("sphere48", ((0, 48),) * 3, (95, 40, 24)),
+               ("sphere48", ((-6, 55),) * 3, (30, 30, 30)),
+               ("blob", ((0, 33), (0, 27), (0, 20)), (50, 13, 20)),
+               ("blob_off", ((0, 45), (-5, 32), (5, 35)), (24, 31, 17))]
+    for i, (rk, gb, res) in enumerate(samples):
+        raw, rb = raws[rk]
+        (X, Y, Z), (x, y, z) = ref.create_grid(gb, res)
+        m = ref.sample_mask_on_grid(raw, (X, Y, Z), bounds_raw=rb)
+        _save(f"mask_sample_{i}", raw=raw, raw_bounds=np.array(rb, dtype=np.float64),
+              raw_bounds_int=int(all(isinstance(v, int) for b in rb for v in b)), ax=x, ay=y, az=z, mask=m)
+    bnd = [("sphere48", 1, 1), ("sphere48", 2, 3), ("blob", 3, 7), ("blob_off", 1, 2), ("blob", 0, 5)]
+    for i, (rk, t, st) in enumerate(bnd):
+        raw, rb = raws[rk]
+        bx, by, bz = ref.extract_boundary_particles(raw, rb, sampling_step=st, thickness=t)
+        _save(f"boundary_{i}", mask=raw, bounds=np.array(rb, dtype=np.float64),
+              bounds_int=int(all(isinstance(v, int) for b in rb for v in b)), thickness=t, step=st,
+              bx=bx, by=by, bz=bz)
+    bx, by, bz = ref.extract_boundary_particles(labels, ((0, 19), (0, 17), (0, 14)), sampling_step=1, thickness=1)
+    _save("boundary_labels", mask=labels, bounds=np.array(((0, 19), (0, 17), (0, 14)), dtype=np.float64),
+          bounds_int=1, thickness=1, step=1, bx=bx, by=by, bz=bz)
+    flat = _blob_mask((1, 20, 30), 3, 8)
+    bx, by, bz = ref.extract_boundary_particles(flat, ((0, 30), (0, 20), (4, 9)), sampling_step=1, thickness=1)
+    _save("boundary_flat", mask=flat, bounds=np.array(((0, 30), (0, 20), (4, 9)), dtype=np.float64),
+          bounds_int=1, thickness=1, step=1, bx=bx, by=by, bz=bz)
+
+
+def filter_cases(ref_path):
+    """remove_outliers_knn (filtering.py:5-58): which particles survive, and the printed radius."""
+    import importlib.util
+
+    # load the reference file explicitly: the repo root holds a `filtering` shim of the same name
+    spec = importlib.util.spec_from_file_location("ref_filtering", os.path.join(ref_path, "filtering.py"))
+    filtering = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(filtering)
+
+    rng = np.random.default_rng(31)
+    n = 4000
+    P = rng.uniform(0, 20, (n, 3))
+    Q = np.stack([np.sin(P[:, 0] / 3), np.cos(P[:, 1] / 4), 0.2 * P[:, 2] / 20], 1) + 0.05 * rng.standard_normal((n, 3))
+    bad = rng.choice(n, 80, replace=False)
+    Q[bad] *= rng.uniform(3, 10, (80, 1))
+    for k, thr in ((25, 3.0), (8, 2.0), (10, 3.0), (63, 3.0)):
+        df = _df(P, Q)
+        df["id"] = np.arange(n)
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            out = filtering.remove_outliers_knn(df, k=k, threshold=thr)
+        keep = np.zeros(n, dtype=bool)
+        keep[out["id"].values] = True
+        _save(f"filter_k{k}_t{thr}", points=P, values=Q, k=k, threshold=thr, keep=keep,
+              stdout=np.array(buf.getvalue()))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
-    ap.add_argument("--only", default="knn,edge,masked,rbf,nearest,div")
+    ap.add_argument("--only", default="knn,edge,masked,rbf,nearest,div,mask,filter")
     a = ap.parse_args()
     ref = _import_reference(a.ref)
     only = a.only.split(",")
@@ -236,6 +317,10 @@ def main():
         nearest_cases(ref)
     if "div" in only:
         div_cases(a.ref)
+    if "mask" in only:
+        mask_cases(ref)
+    if "filter" in only:
+        filter_cases(a.ref)
 
 
 if __name__ == "__main__":

@@ -77,6 +77,7 @@ def test_load_ptv_data_renames(tmp_path):
         ip.load_ptv_data(str(bad))
 
 
+@pytest.mark.gpu
 def test_mask_sampling_and_boundary_particles_match_reference():
     g = load("masked_spherepack_idw")
     fluid = g["fluid_raw"]

@@ -116,3 +116,42 @@ def test_nearest_oracle_matches_reference():
     U, V, W = cpu_ref.interp_grid(g["points"], g["values"], g["ax"], g["ay"], g["az"], "nearest")
     for a, b in ((U, g["U"]), (V, g["V"]), (W, g["W"])):
         assert np.array_equal(a, b)
+
+
+# ------------------------------------------------ pore-mask path + outlier filter (§8(f) rows 2-3)
+def _bounds(g, key):
+    b = g[key]
+    if int(g[key + "_int"]):
+        b = b.astype(int)
+    return tuple(tuple(v.tolist()) for v in b)
+
+
+@pytest.mark.parametrize("name", names(("mask_sample_",)))
+def test_oracle_sample_mask_matches_reference(name):
+    g = load(name)
+    Z, Y, X = np.meshgrid(g["az"], g["ay"], g["ax"], indexing="ij")
+    assert np.array_equal(cpu_ref.sample_mask_nearest(g["raw"], _bounds(g, "raw_bounds"), X, Y, Z), g["mask"])
+
+
+@pytest.mark.parametrize("name", names(("boundary_",)))
+def test_oracle_boundary_particles_match_reference(name):
+    g = load(name)
+    got = cpu_ref.boundary_particles(g["mask"], _bounds(g, "bounds"), int(g["step"]), int(g["thickness"]))
+    for a, e in zip(got, (g["bx"], g["by"], g["bz"])):
+        assert a.dtype == e.dtype and np.array_equal(a, e)
+
+
+@pytest.mark.parametrize("name", names(("filter_",)))
+def test_oracle_outlier_filter_matches_reference(name):
+    g = load(name)
+    keep, radius = cpu_ref.outlier_filter(g["points"], g["values"], int(g["k"]), float(g["threshold"]))
+    assert np.array_equal(keep, g["keep"])
+    assert f"= {radius:.4f}\n" in str(g["stdout"])
+
+
+def test_oracle_rgi_nearest_tie_and_bounds():
+    g = np.array([0.0, 1.0, 2.0, 3.0])
+    x = np.array([-0.1, 0.0, 0.5, 0.5000001, 1.5, 2.9, 3.0, 3.1])
+    assert cpu_ref.rgi_nearest_index(g, x).tolist() == [-1, 0, 0, 1, 1, 3, 3, -1]
+    assert cpu_ref.rgi_nearest_index(g[::-1], x).tolist() == [-1, 3, 3, 2, 2, 0, 0, -1]
+    assert cpu_ref.rgi_nearest_index(np.array([2.0]), np.array([2.0, 2.5])).tolist() == [0, -1]
