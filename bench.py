@@ -43,6 +43,9 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Mvoxels/s interpolated + achieved HBM GB/s, 512³ grid / 5M particles IDW"
 METRIC_DIV = "Mvoxels/s + achieved HBM GB/s, consistent divergence (physics.py:6-53) of a 512³ field"
+METRIC_FILTER = "Mparticles/s filtered + achieved HBM GB/s, k-NN median/MAD outlier filter (filtering.py:5-58), 5M particles"
+METRIC_MASK = ("Mvoxels/s + achieved HBM GB/s, pore-mask path (sample_mask_on_grid + extract_boundary_particles, "
+               "interpolator.py:205-284), 512³ mask")
 METRIC_RBF = "Mvoxels/s interpolated + achieved FP64 TFLOP/s, 512³ grid / 5M particles local RBF"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec (AMD); not listed in the guide
@@ -75,7 +78,7 @@ def parse():
     ap.add_argument("--particles", type=int, default=5_000_000)
     ap.add_argument("--k", type=int, default=8)
     ap.add_argument("--power", type=float, default=2.0)
-    ap.add_argument("--method", default="idw", choices=["idw", "sibson", "nearest", "rbf", "div"])
+    ap.add_argument("--method", default="idw", choices=["idw", "sibson", "nearest", "rbf", "div", "filter", "mask"])
     ap.add_argument("--div-dtype", default="f64", choices=["f64", "f32"],
                     help="--method div: field dtype (f32 = the C5 fp32 field, Python-float spacings)")
     ap.add_argument("--rbf-kernel", default="thin_plate_spline", help="--method rbf: scipy kernel name")
@@ -284,10 +287,216 @@ def main_div(args):
         dist.destroy_process_group()
 
 
+def _dist_init():
+    """One process per GPU (torchrun env); returns (world, rank, local, dist or None, device)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local, dist, torch.device("cuda", local)
+
+
+def _timed(step, args, dist, dev, stat_key, ctx):
+    """W warmup steps, then K steps between barriers + synchronize; (max-over-ranks seconds, kernel ms list)."""
+    import torch
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    k_ms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        k_ms.append(ctx.last_stats()[stat_key] if stat_key else 0.0)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, k_ms
+
+
+def main_filter(args):
+    """--method filter: one step = remove_outliers_knn (filtering.py:5-58) over a resident particle set:
+    binning + (k+1)-NN of every particle among the particles (slot mode) + median/MAD per particle.
+    Weak scaling: each rank filters its own sphere-pack copy (independent particle sets)."""
+    import torch
+
+    world, rank, local, dist, dev = _dist_init()
+    from ptv_interpolation_amd import _lib, synth
+
+    k = 25 if args.k == 8 else args.k   # the reference default (main.py:44)
+    P, _ = synth.sphere_pack(args.particles, args.grid)
+    rng = np.random.default_rng(20260214 + rank)
+    Q = rng.standard_normal((len(P), 3))
+    Q[rng.choice(len(P), len(P) // 100, replace=False)] *= 8.0  # 1 % outliers
+    n = len(P)
+    cols = [torch.from_numpy(np.ascontiguousarray(P[:, i])).to(dev) for i in range(3)] + \
+           [torch.from_numpy(np.ascontiguousarray(Q[:, i])).to(dev) for i in range(3)]
+    keep = torch.empty(n, dtype=torch.uint8, device=dev)
+    kth = torch.empty(n, dtype=torch.float64, device=dev)
+    ctx = _lib.Context(local)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        return ctx.filter_outliers_knn_dev(n, [c.data_ptr() for c in cols], keep.data_ptr(), kth.data_ptr(), k=k,
+                                           threshold=3.0, stream=stream)
+
+    elapsed, k_ms = _timed(step, args, dist, dev, "ms_knn", ctx)
+    st = ctx.last_stats()
+    kavg = float(np.mean(k_ms))
+    # gather model (SURVEY §8(d)) per particle: k+1 neighbour records {x,y,z,u,v,w} + keep byte + k-th distance
+    alg = n * ((6 * (k + 1)) * 8 + 1 + 8)
+    ach = alg / (kavg * 1e-3) / 1e9
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            from oracle import cpu_ref
+
+            m = min(n, 400_000)
+            t = time.perf_counter()
+            cpu_ref.outlier_filter(P[:m], Q[:m], k, 3.0, workers=1)
+            dt = time.perf_counter() - t
+            cpu = {"value": round(m / dt / 1e6, 4), "unit": "Mparticles/s", "cores": 1, "kind": "port",
+                   "sample": f"first {m} particles of the same cloud (a {m / n:.0%} subset at the same density "
+                             "is not the same neighbourhoods; documented), scipy KDTree(k+1) + numpy median/MAD "
+                             "(oracle/cpu_ref.outlier_filter = filtering.py:15-51), workers=1",
+                   "seconds": round(dt, 2)}
+        except Exception as e:
+            cpu = {"value": None, "error": repr(e)[:200]}
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC_FILTER, "value": round(n * world / (elapsed / args.steps) / 1e6, 2),
+            "unit": "Mparticles/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic: generate_sphere_pack.py geometry, N(0,1) velocities with 1% x8 outliers",
+            "config": {"workload": f"remove_outliers_knn k={k} threshold=3 over {n} particles", "k": k,
+                       "particles": n, "method": "filter", "parallelism": f"independent particle sets x{world}"},
+            "breakdown_ms": {"bin": round(st["ms_bin"], 3), "knn+stats": round(kavg, 3)},
+            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
+                         "kernel": f"k_knn_interp<{32 if k + 1 <= 32 else 64}> (slot mode) + k_outlier_stats",
+                         "alg_bytes_per_launch": alg, "kernel_ms": round(kavg, 4)},
+            "cpu_baseline": cpu}), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def main_mask(args):
+    """--method mask: one step = sample_mask_on_grid (a G^3 raw mask onto the G^3 grid, main.py:161
+    at --downscale 1) + extract_boundary_particles(thickness=1, step=1) (main.py:168) on resident
+    bytes.  Weak scaling: each rank processes its own mask copy."""
+    import torch
+
+    world, rank, local, dist, dev = _dist_init()
+    from ptv_interpolation_amd import _lib, synth
+
+    G = args.grid
+    fluid = synth.fluid_mask(G)
+    raw = torch.from_numpy(np.ascontiguousarray(fluid).view(np.uint8)).to(dev)
+    ax_h = np.linspace(0, G - 1, G)
+    axes = [torch.from_numpy(ax_h.copy()).to(dev) for _ in range(3)]
+    out = torch.empty((G, G, G), dtype=torch.uint8, device=dev)
+    ctx = _lib.Context(local)
+    # a real (non-null) torch stream, so that the library's launches and the timing events share it
+    torch.cuda.set_stream(torch.cuda.Stream(dev))
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    lo, span, den = [0.0] * 3, [float(G - 1)] * 3, [float(G - 1)] * 3
+    nb = ctx.boundary_particles_dev(raw.data_ptr(), (G, G, G), 1, 1, lo, span, den, stream=stream)
+    bxyz = torch.empty((3, max(nb, 1)), dtype=torch.float64, device=dev)
+    optrs = [bxyz[i].data_ptr() for i in range(3)]
+    ms = {"sample": [], "boundary": []}
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+
+    def step():
+        e[0].record()
+        ctx.sample_mask_dev(raw.data_ptr(), (G, G, G), (ax_h, ax_h, ax_h), [a.data_ptr() for a in axes],
+                            (G, G, G), out.data_ptr(), stream=stream)
+        e[1].record()
+        ctx.boundary_particles_dev(raw.data_ptr(), (G, G, G), 1, 1, lo, span, den, out_ptrs=optrs, cap=nb,
+                                   stream=stream)
+        e[2].record()
+
+    def step_timed():
+        step()
+        torch.cuda.synchronize(dev)
+        ms["sample"].append(e[0].elapsed_time(e[1]))
+        ms["boundary"].append(e[1].elapsed_time(e[2]))
+
+    elapsed, _ = _timed(step_timed, args, dist, dev, None, ctx)
+    V = G ** 3
+    t_s, t_b = float(np.mean(ms["sample"][args.warmup:] or ms["sample"])), float(np.mean(ms["boundary"][args.warmup:] or ms["boundary"]))
+    alg_s = 2 * V            # read the raw byte, write the grid byte (same resolution)
+    alg_b = V + 24 * nb      # read the mask once, write 3 doubles per boundary particle
+    ach_s = alg_s / (t_s * 1e-3) / 1e9
+    ach_b = alg_b / (t_b * 1e-3) / 1e9
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            from oracle import cpu_ref
+
+            Gs = min(G, 256)
+            f = synth.fluid_mask(Gs)
+            (X, Y, Z) = np.meshgrid(np.linspace(0, Gs - 1, Gs), np.linspace(0, Gs - 1, Gs),
+                                    np.linspace(0, Gs - 1, Gs), indexing="ij")[::-1]
+            t = time.perf_counter()
+            cpu_ref.sample_mask_nearest(f, ((0, Gs),) * 3, X, Y, Z)
+            cpu_ref.boundary_particles(f, ((0, Gs),) * 3, 1, 1)
+            dt = time.perf_counter() - t
+            cpu = {"value": round(Gs ** 3 / dt / 1e6, 3), "unit": "Mvoxels/s", "cores": 1, "kind": "port",
+                   "sample": f"{Gs}^3 sphere-pack mask, numpy restatement (oracle/cpu_ref.sample_mask_nearest + "
+                             "boundary_particles of interpolator.py:205-284), 1 process",
+                   "seconds": round(dt, 2)}
+        except Exception as ex:
+            cpu = {"value": None, "error": repr(ex)[:200]}
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC_MASK, "value": round(V * world / (elapsed / args.steps) / 1e6, 2),
+            "unit": "Mvoxels/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic: generate_sphere_pack.py fluid mask at voxel centres",
+            "config": {"workload": f"sample_mask_on_grid {G}^3 -> {G}^3 + extract_boundary_particles "
+                                   f"(thickness 1, step 1, {nb} particles)", "grid": G, "method": "mask",
+                       "parallelism": f"independent masks x{world}"},
+            "breakdown_ms": {"sample": round(t_s, 4), "boundary": round(t_b, 4)},
+            "roofline": {"bound": "hbm", "achieved": round(ach_b, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(ach_b / HBM_PEAK_GBPS, 4), "traffic": None,
+                         "kernel": "extract_boundary_particles (k_boundary_count + scan + k_boundary_emit)",
+                         "alg_bytes_per_launch": alg_b, "kernel_ms": round(t_b, 4),
+                         "sample_mask": {"achieved": round(ach_s, 1), "frac": round(ach_s / HBM_PEAK_GBPS, 4),
+                                         "alg_bytes": alg_s, "kernel_ms": round(t_s, 4)}},
+            "cpu_baseline": cpu}), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     if args.method == "div":
         return main_div(args)
+    if args.method == "filter":
+        return main_filter(args)
+    if args.method == "mask":
+        return main_mask(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

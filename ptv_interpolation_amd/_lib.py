@@ -310,6 +310,42 @@ class Context:
         self.stats = st.as_dict()
         return keep, kth
 
+    # device-pointer variants (bench.py: inputs resident in HBM)
+    def sample_mask_dev(self, raw_ptr, raw_shape, raw_axes, axes_ptrs, shape, out_ptr, stream=None):
+        """raw_ptr: device (rnz, rny, rnx) bytes; raw_axes: host arrays; axes_ptrs: device grid axes."""
+        rnz, rny, rnx = raw_shape
+        rax, ray, raz = (np.ascontiguousarray(a, dtype=np.float64).ravel() for a in raw_axes)
+        M = MaskGrid(rnx, rny, rnz, C.cast(C.c_void_p(raw_ptr), _u8p), as_dp(rax), as_dp(ray), as_dp(raz))
+        nz, ny, nx = shape
+        G = Grid(nx, ny, nz, dev_dp(axes_ptrs[0]), dev_dp(axes_ptrs[1]), dev_dp(axes_ptrs[2]), None, None, None,
+                 0, nz)
+        check(lib().ptv_sample_mask_dev(self.h, C.byref(M), C.byref(G), C.cast(C.c_void_p(out_ptr), _u8p),
+                                        C.c_void_p(stream) if stream else None))
+
+    def boundary_particles_dev(self, mask_ptr, shape, thickness, step, lo, span, den, out_ptrs=None, cap=0,
+                               stream=None, encoding=MASK_BOOL):
+        """Returns the particle count; writes device x, y, z when out_ptrs is given and cap suffices."""
+        nz, ny, nx = shape
+        prm = BoundaryParams(nx, ny, nz, C.cast(C.c_void_p(mask_ptr), _u8p), int(encoding), int(thickness),
+                             int(step), (C.c_double * 3)(*lo), (C.c_double * 3)(*span), (C.c_double * 3)(*den))
+        cnt = C.c_int64(0)
+        o = [dev_dp(p) for p in out_ptrs] if out_ptrs else [None, None, None]
+        check(lib().ptv_boundary_particles_dev(self.h, C.byref(prm), o[0], o[1], o[2], int(cap), C.byref(cnt),
+                                               C.c_void_p(stream) if stream else None))
+        return cnt.value
+
+    def filter_outliers_knn_dev(self, n, col_ptrs, keep_ptr, kth_ptr, k=25, threshold=3.0, mad_eps=1e-6,
+                                stream=None):
+        """col_ptrs: six device float64 columns x, y, z, u, v, w."""
+        P = Particles(int(n), *[dev_dp(p) for p in col_ptrs])
+        prm = FilterParams(int(k), float(threshold), float(mad_eps))
+        st = Stats()
+        check(lib().ptv_filter_outliers_knn_dev(self.h, C.byref(P), C.byref(prm),
+                                                C.cast(C.c_void_p(keep_ptr), _u8p),
+                                                dev_dp(kth_ptr) if kth_ptr else None,
+                                                C.c_void_p(stream) if stream else None, C.byref(st)))
+        return st.as_dict()
+
     # -- host buffers ------------------------------------------------------
     def interp_knn(self, points, values, axes=None, grid_points=None, shape=None, method=METHOD_IDW, k=8,
                    power=2.0, eps=1e-10, fluid_mask=None, flags=0, z_range=None, cell_occupancy=0.0,

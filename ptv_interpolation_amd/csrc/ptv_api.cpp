@@ -79,6 +79,8 @@ struct ptv_ctx {
     DevBuf<unsigned long long> bnd_counts;                       // boundary: per-block counts / offsets
     DevBuf<double> bnd_xyz;                                      // boundary host calls: coordinates
     DevBuf<uint8_t> flt_keep;                                    // outlier filter host calls
+    DevBuf<uint32_t> flt_code, flt_perm, flt_count, flt_start, flt_scanp;  // filter: query bricks
+    DevBuf<double4> flt_prec, flt_pval;
     DevBuf<double> flt_kth;
     hipEvent_t ev_div0 = nullptr, ev_div1 = nullptr;             // around the divergence stencil
     bool div_pending = false;
@@ -191,6 +193,9 @@ int ptv_free(ptv_ctx *c) {
     c->bnd_counts.release();
     c->bnd_xyz.release();
     c->flt_keep.release();
+    for (auto *b : {&c->flt_code, &c->flt_perm, &c->flt_count, &c->flt_start, &c->flt_scanp}) b->release();
+    c->flt_prec.release();
+    c->flt_pval.release();
     c->flt_kth.release();
     hipEventDestroy(c->ev_div0);
     hipEventDestroy(c->ev_div1);
@@ -1205,8 +1210,23 @@ int run_filter(ptv_ctx *c, const ptv_particles *p, const ptv_filter_params *prm,
     KnnLaunch kl;
     Binned b{};
     PTV_TRY(prepare(c, p, &g, &sp, nullptr, nullptr, nullptr, g.px, g.py, g.pz, s, kl, b));
-    // the binned order as the query order: a wave's 64 queries are 64 neighbouring records
-    PTV_TRY(launch_binned_queries(b.prec, n, npad, c->qpts[0].p, c->qpts[1].p, c->qpts[2].p, s));
+    // query order: a counting sort into bricks of ~64 particles (a wave's queries are one
+    // compact blob), over the bounding box prepare() measured
+    const double lo[3] = {c->h_bbox[0], c->h_bbox[1], c->h_bbox[2]};
+    const double hi[3] = {c->h_bbox[3], c->h_bbox[4], c->h_bbox[5]};
+    const CellGrid qg = make_cell_grid(lo, hi, n, 64.0);
+    const size_t qm = (size_t)qg.ncells;
+    PTV_TRY(c->flt_code.ensure(n));
+    PTV_TRY(c->flt_perm.ensure(n));
+    PTV_TRY(c->flt_prec.ensure(n));
+    PTV_TRY(c->flt_pval.ensure(n));
+    PTV_TRY(c->flt_count.ensure(qm));
+    PTV_TRY(c->flt_start.ensure(qm + 1));
+    PTV_TRY(c->flt_scanp.ensure(scan_partials_needed(qm) + 1));
+    const double *pp[3] = {p->x, p->y, p->z}, *pv[3] = {p->u, p->v, p->w};
+    PTV_TRY(launch_bin(qg, pp, pv, n, c->flt_code.p, c->flt_perm.p, c->flt_count.p, c->flt_start.p, c->flt_scanp.p,
+                       c->flt_prec.p, c->flt_pval.p, s));
+    PTV_TRY(launch_binned_queries(c->flt_prec.p, n, npad, c->qpts[0].p, c->qpts[1].p, c->qpts[2].p, s));
     PTV_TRY(c->slots.ensure((size_t)npad * (prm->k + 1)));
     kl.mode = kModeSlots;
     kl.slots = c->slots.p;
@@ -1214,7 +1234,7 @@ int run_filter(ptv_ctx *c, const ptv_particles *p, const ptv_filter_params *prm,
     PTV_TRY(launch_knn(kl, b, nullptr, nullptr, nullptr, c->qpts[0].p, c->qpts[1].p, c->qpts[2].p, nullptr, nullptr,
                        nullptr, nullptr, s));
     FilterArgs fa{n, prm->k, prm->threshold, prm->mad_eps};
-    PTV_TRY(launch_outlier_stats(fa, b, c->slots.p, keep, kth, s));
+    PTV_TRY(launch_outlier_stats(fa, b, c->flt_prec.p, c->flt_pval.p, c->slots.p, keep, kth, s));
     PTV_HIP(hipEventRecord(c->ev_knn1, s));
     c->timed_pending = true;
     c->last.n_voxels = n;

@@ -8,15 +8,17 @@
 //   keep = |speed - med| / (mad + 1e-6) <= threshold                   (:47-51)
 //
 // The (k+1)-NN query runs on the same k-NN kernel as the grid path (slot mode, the
-// particles themselves as a point-list "grid" in binned order so that a wave's 64 queries
-// share cells).  This file holds the two thin kernels either side of it: building the
-// binned query list, and the per-particle statistics.
+// particles themselves as a point-list "grid").  The query order is a second counting
+// sort of the particles into coarse bricks of ~64 particles, so that a wave's 64 queries
+// form a compact blob (the search-cell order would make them a thin strip along x, whose
+// gather box is ~10x larger).  This file holds the two thin kernels either side of the
+// search: building the query list, and the per-particle statistics.
 #include "ptv_api.h"
 #include "ptv_kernels.hpp"
 
 namespace ptv {
 
-// queries in binned (cell) order, padded to `npad` with the last record
+// queries in brick order, padded to `npad` with the last record
 __global__ __launch_bounds__(256) void k_binned_queries(const double4 *__restrict__ prec, int64_t n, int64_t npad,
                                                         double *__restrict__ qx, double *__restrict__ qy,
                                                         double *__restrict__ qz) {
@@ -85,12 +87,14 @@ __device__ __forceinline__ double speed_of(const double4 v) {
 template <int KMAX>
 __global__ __launch_bounds__(256) void k_outlier_stats(FilterArgs a, const double4 *__restrict__ prec,
                                                        const double4 *__restrict__ pval,
+                                                       const double4 *__restrict__ qrec,
+                                                       const double4 *__restrict__ qval,
                                                        const uint32_t *__restrict__ slots, uint8_t *__restrict__ keep,
                                                        double *__restrict__ kth) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= a.n) return;
     const int k1 = a.k + 1;
-    const double4 q = prec[i];
+    const double4 q = qrec[i];  // query i (brick order); .w = original index
     const uint32_t *sl = slots + (size_t)i * k1;
     // the point itself is column 0 of the reference query (distance 0); when several
     // particles coincide with it, the query point's own record is the one dropped
@@ -109,7 +113,7 @@ __global__ __launch_bounds__(256) void k_outlier_stats(FilterArgs a, const doubl
                 drop = j;
             }
             dmax = fmax(dmax, d);
-            if ((int64_t)s == i) self = j;
+            if (r.w == q.w) self = j;  // the same particle (original index)
         }
     }
     if (self >= 0) drop = self;  // at distance 0 == dmin whenever it is in the list
@@ -132,7 +136,7 @@ __global__ __launch_bounds__(256) void k_outlier_stats(FilterArgs a, const doubl
 #pragma unroll
     for (int t = 0; t < KMAX; ++t) dev[t] = fabs(sp[t] - med);
     const double mad = median_of(dev, a.k);
-    const double z = fabs(speed_of(pval[i]) - med) / (mad + a.mad_eps);
+    const double z = fabs(speed_of(qval[i]) - med) / (mad + a.mad_eps);
     const int64_t orig = (int64_t)q.w;
     keep[orig] = z <= a.threshold ? 1 : 0;
     if (kth) kth[orig] = dmax;
@@ -162,14 +166,14 @@ int launch_pad_queries(const double *x, const double *y, const double *z, int64_
     return PTV_OK;
 }
 
-int launch_outlier_stats(const FilterArgs &a, const Binned &b, const uint32_t *slots, uint8_t *keep, double *kth,
-                         hipStream_t s) {
+int launch_outlier_stats(const FilterArgs &a, const Binned &b, const double4 *qrec, const double4 *qval,
+                         const uint32_t *slots, uint8_t *keep, double *kth, hipStream_t s) {
     const dim3 grid((unsigned)((a.n + 255) / 256));
     switch (filter_kmax(a.k)) {
-        case 8: hipLaunchKernelGGL(k_outlier_stats<8>, grid, dim3(256), 0, s, a, b.prec, b.pval, slots, keep, kth); break;
-        case 16: hipLaunchKernelGGL(k_outlier_stats<16>, grid, dim3(256), 0, s, a, b.prec, b.pval, slots, keep, kth); break;
-        case 32: hipLaunchKernelGGL(k_outlier_stats<32>, grid, dim3(256), 0, s, a, b.prec, b.pval, slots, keep, kth); break;
-        case 64: hipLaunchKernelGGL(k_outlier_stats<64>, grid, dim3(256), 0, s, a, b.prec, b.pval, slots, keep, kth); break;
+        case 8: hipLaunchKernelGGL(k_outlier_stats<8>, grid, dim3(256), 0, s, a, b.prec, b.pval, qrec, qval, slots, keep, kth); break;
+        case 16: hipLaunchKernelGGL(k_outlier_stats<16>, grid, dim3(256), 0, s, a, b.prec, b.pval, qrec, qval, slots, keep, kth); break;
+        case 32: hipLaunchKernelGGL(k_outlier_stats<32>, grid, dim3(256), 0, s, a, b.prec, b.pval, qrec, qval, slots, keep, kth); break;
+        case 64: hipLaunchKernelGGL(k_outlier_stats<64>, grid, dim3(256), 0, s, a, b.prec, b.pval, qrec, qval, slots, keep, kth); break;
         default:
             set_error("outlier filter: k must be <= 63 (k + 1 neighbours on the GPU k-NN list)");
             return PTV_E_UNSUPPORTED;

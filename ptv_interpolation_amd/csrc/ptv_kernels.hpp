@@ -152,7 +152,8 @@ int launch_pad_queries(const double *x, const double *y, const double *z, int64_
                        double *qy, double *qz, hipStream_t s);
 int launch_binned_queries(const double4 *prec, int64_t n, int64_t npad, double *qx, double *qy, double *qz,
                           hipStream_t s);
-int launch_outlier_stats(const FilterArgs &a, const Binned &b, const uint32_t *slots, uint8_t *keep, double *kth,
-                         hipStream_t s);
+// qrec/qval: the query particles (records {x,y,z,original index}, values) in query order
+int launch_outlier_stats(const FilterArgs &a, const Binned &b, const double4 *qrec, const double4 *qval,
+                         const uint32_t *slots, uint8_t *keep, double *kth, hipStream_t s);
 
 }  // namespace ptv

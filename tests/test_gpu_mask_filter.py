@@ -202,3 +202,20 @@ def test_outlier_filter_full_size_properties(ctx):
     exp = np.abs(speed[sel] - med) / (mad + 1e-6) <= 3.0
     assert np.array_equal(keep.view(bool)[sel], exp)
     assert np.array_equal(kth[sel], dist[:, -1])
+
+
+@pytest.mark.parametrize("thickness", [1, 2])
+def test_boundary_particles_label_mask_aligned_rows(ctx, thickness):
+    """Integer label mask with 16-aligned rows (the 16-voxel SWAR kernels) and the numpy
+    `bool & ~int` low-bit rule, against the oracle; also a bool mask of the same shape."""
+    from ptv_interpolation_amd import interpolator as ip
+
+    rng = np.random.default_rng(40 + thickness)
+    lab = rng.integers(0, 4, (12, 10, 32)).astype(np.uint8)
+    lab[:, :, 8:20] = 0
+    b = ((0, 32), (0, 10), (0, 12))
+    for m in (lab, lab == 2):
+        got = ip.extract_boundary_particles(m, b, sampling_step=1, thickness=thickness)
+        exp = cpu_ref.boundary_particles(m, b, 1, thickness)
+        for a, e in zip(got, exp):
+            assert np.array_equal(a, e)
