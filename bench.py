@@ -84,6 +84,9 @@ def parse():
     ap.add_argument("--rbf-kernel", default="thin_plate_spline", help="--method rbf: scipy kernel name")
     ap.add_argument("--epsilon", type=float, default=None, help="--method rbf: shape parameter")
     ap.add_argument("--degree", type=int, default=None, help="--method rbf: polynomial degree")
+    ap.add_argument("--out-dtype", default="f64", choices=["f64", "f32"],
+                    help="k-NN methods: U, V, W stored as float32 (PTV_FLAG_OUT_F32, the fused main.py:230 "
+                         "astype; arithmetic stays f64) — the C5 configuration's field")
     ap.add_argument("--halo", type=int, default=64, help="neighbour-copy halo (voxels) for N>1")
     ap.add_argument("--cpu-sample-planes", type=int, default=16)
     ap.add_argument("--cpu-workers", type=int, default=16)
@@ -524,7 +527,8 @@ def main():
     cols = [torch.from_numpy(np.ascontiguousarray(P[:, i])).to(dev) for i in range(3)] + \
            [torch.from_numpy(np.ascontiguousarray(Q[:, i])).to(dev) for i in range(3)]
     axes = [torch.from_numpy(ax_h).to(dev), torch.from_numpy(ax_h.copy()).to(dev), torch.from_numpy(az_h).to(dev)]
-    out = [torch.empty((G, G, G), dtype=torch.float64, device=dev) for _ in range(3)]
+    out_f32 = args.out_dtype == "f32" and args.method != "rbf"
+    out = [torch.empty((G, G, G), dtype=torch.float32 if out_f32 else torch.float64, device=dev) for _ in range(3)]
     ctx = _lib.Context(local)
     method = {"idw": _lib.METHOD_IDW, "sibson": _lib.METHOD_SIBSON, "nearest": _lib.METHOD_NEAREST}.get(args.method)
     if args.method == "nearest":
@@ -544,7 +548,8 @@ def main():
             return ctx.interp_knn_dev(n, [c.data_ptr() for c in cols], G, G, G,
                                       axes_ptrs=[a.data_ptr() for a in axes],
                                       out_ptrs=[o.data_ptr() for o in out], method=method, k=args.k,
-                                      power=args.power, stream=stream)
+                                      power=args.power, stream=stream,
+                                      flags=_lib.FLAG_OUT_F32 if out_f32 else 0)
 
     for _ in range(args.warmup):
         step()
@@ -573,7 +578,7 @@ def main():
 
     gather_ms = None
     if args.allgather and dist is not None:
-        full = [torch.empty((G * world, G, G), dtype=torch.float64, device=dev) for _ in range(3)]
+        full = [torch.empty((G * world, G, G), dtype=out[0].dtype, device=dev) for _ in range(3)]
         torch.cuda.synchronize(dev)
         dist.barrier()
         tg = time.perf_counter()
@@ -587,7 +592,7 @@ def main():
     ms_step = elapsed / args.steps * 1e3
     value = vox * world / (elapsed / args.steps) / 1e6
     knn_avg = float(np.mean(knn_ms))
-    alg_bytes = vox * (6 * args.k + 3) * 8
+    alg_bytes = vox * ((6 * args.k) * 8 + 3 * (4 if out_f32 else 8))
     achieved = alg_bytes / (knn_avg * 1e-3) / 1e9
     traffic = traffic_from_profiles()
 
@@ -629,7 +634,8 @@ def main():
                                     f"eps={eps} degree={deg} (system {m_sys}) fp64 (z-slab per GPU)")
                        if args.method == "rbf" else
                        f"{G}^3 grid / {args.particles} particles {args.method.upper()} "
-                       f"k={args.k} p={args.power} fp64 (z-slab per GPU)",
+                       f"k={args.k} p={args.power} fp64" + (" (float32 U, V, W)" if out_f32 else "") +
+                       " (z-slab per GPU)",
                        "grid": G, "particles": args.particles, "particles_binned_rank0": n,
                        "method": args.method, "k": args.k, "power": args.power,
                        "parallelism": f"z-slab x{world}"},

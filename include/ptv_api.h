@@ -52,6 +52,10 @@ extern "C" {
 
 /* flags for ptv_knn_params.flags / ptv_rbf_params.flags */
 #define PTV_FLAG_NAN_TO_NUM 1u  /* fused main.py:195-199 nan_to_num on the outputs */
+/* k-NN methods: write U, V, W as float32 (the buffers passed as `double *` then hold float):
+ * the fused `U.astype(np.float32)` of main.py:230, applied after the float64 result, the
+ * nan_to_num and the mask (half the output bytes).  Arithmetic stays float64. */
+#define PTV_FLAG_OUT_F32 2u
 
 typedef struct ptv_ctx ptv_ctx;
 

@@ -69,6 +69,7 @@ class RbfParams(C.Structure):
 
 F64 = 0
 F32 = 1
+FLAG_OUT_F32 = 2  # U, V, W written as float32 (main.py:230 astype, fused)
 
 
 class DivParams(C.Structure):
@@ -375,7 +376,8 @@ class Context:
         prm = KnnParams(method, int(k), float(power), float(eps),
                         mk.ctypes.data_as(C.POINTER(C.c_uint8)) if mk is not None else None, flags,
                         float(cell_occupancy), float(r0_scale), int(lattice_bounds))
-        out = [np.empty((z1 - z0, ny, nx), dtype=np.float64) for _ in range(3)]
+        odt = np.float32 if flags & FLAG_OUT_F32 else np.float64
+        out = [np.empty((z1 - z0, ny, nx), dtype=odt) for _ in range(3)]
         st = Stats()
         check(lib().ptv_interp_knn(self.h, C.byref(P), C.byref(G), C.byref(prm),
                                    as_dp(out[0]), as_dp(out[1]), as_dp(out[2]), C.byref(st)))

@@ -550,6 +550,10 @@ std::vector<int> monomial_powers(int degree) {
 }
 
 int validate_rbf(const ptv_particles *p, const ptv_rbf_params *prm, int *m_out) {
+    if (prm->flags & PTV_FLAG_OUT_F32) {
+        set_error("local RBF: PTV_FLAG_OUT_F32 is supported by the k-NN methods only");
+        return PTV_E_UNSUPPORTED;
+    }
     if (prm->kernel < PTV_RBF_LINEAR || prm->kernel > PTV_RBF_GAUSSIAN) {
         set_error("unknown RBF kernel " + std::to_string(prm->kernel));
         return PTV_E_ARG;
@@ -702,7 +706,7 @@ struct EventSet {
 // the slab's three output planes, timings.  compute(dp, dg, dmask, dsmooth, U, V, W, s).
 template <typename F>
 int host_call(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const uint8_t *mask_h, const double *smooth_h,
-              double *U, double *V, double *W, F &&compute) {
+              double *U, double *V, double *W, F &&compute, size_t out_elem = sizeof(double)) {
     hipStream_t s = c->stream;
     EventSet ev;
     for (hipEvent_t &e : ev.e) PTV_HIP(hipEventCreate(&e));
@@ -757,7 +761,7 @@ int host_call(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const uint8
     PTV_HIP(hipEventRecord(ev.e[2], s));
     double *dst[3] = {U, V, W};
     for (int i = 0; i < 3; ++i)
-        PTV_HIP(hipMemcpyAsync(dst[i], c->out[i].p, nvox * sizeof(double), hipMemcpyDeviceToHost, s));
+        PTV_HIP(hipMemcpyAsync(dst[i], c->out[i].p, nvox * out_elem, hipMemcpyDeviceToHost, s));
     PTV_HIP(hipEventRecord(ev.e[3], s));
     PTV_HIP(hipStreamSynchronize(s));
     PTV_TRY(finish_timing(c));
@@ -867,7 +871,8 @@ int ptv_interp_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const 
                           double *dU, double *dV, double *dW, hipStream_t s) {
                           return run_knn(c, dp, dg, prm, dg->ax, dg->ay, dg->az, dg->px, dg->py, dg->pz, dmask, dU,
                                          dV, dW, s, nullptr);
-                      }));
+                      },
+                      (prm->flags & PTV_FLAG_OUT_F32) ? sizeof(float) : sizeof(double)));
     if (st) *st = c->last;
     return PTV_OK;
 }
@@ -1206,15 +1211,19 @@ int run_filter(ptv_ctx *c, const ptv_particles *p, const ptv_filter_params *prm,
     g.pz = c->qpts[2].p;
     g.z_begin = 0;
     g.z_end = g.nz;
-    const SearchParams sp{PTV_METHOD_IDW, prm->k + 1, 2.0, 1e-10, 0u, 0.0, 0.0, -1};
+    double r0s = 0.0, occ = 0.0, brick = 32.0;  // brick 32: 87.5 ms vs 92.4 at 64 (5M, k = 25)
+    if (const char *e = std::getenv("PTV_FILTER_R0")) r0s = std::atof(e);       // dev knobs
+    if (const char *e = std::getenv("PTV_FILTER_OCC")) occ = std::atof(e);
+    if (const char *e = std::getenv("PTV_FILTER_BRICK")) brick = std::atof(e);
+    const SearchParams sp{PTV_METHOD_IDW, prm->k + 1, 2.0, 1e-10, 0u, occ, r0s, -1};
     KnnLaunch kl;
     Binned b{};
     PTV_TRY(prepare(c, p, &g, &sp, nullptr, nullptr, nullptr, g.px, g.py, g.pz, s, kl, b));
-    // query order: a counting sort into bricks of ~64 particles (a wave's queries are one
+    // query order: a counting sort into bricks of ~32 particles (a wave's queries are one
     // compact blob), over the bounding box prepare() measured
     const double lo[3] = {c->h_bbox[0], c->h_bbox[1], c->h_bbox[2]};
     const double hi[3] = {c->h_bbox[3], c->h_bbox[4], c->h_bbox[5]};
-    const CellGrid qg = make_cell_grid(lo, hi, n, 64.0);
+    const CellGrid qg = make_cell_grid(lo, hi, n, brick);
     const size_t qm = (size_t)qg.ncells;
     PTV_TRY(c->flt_code.ensure(n));
     PTV_TRY(c->flt_perm.ensure(n));

@@ -175,6 +175,20 @@ __device__ __forceinline__ double sqrt_cr(double x) {
     return fma(fma(-g, g, x), h, g);
 }
 
+// one voxel's outputs: float64, or float32 (RNE, numpy astype) under PTV_FLAG_OUT_F32
+__device__ __forceinline__ void store_out(uint32_t flags, double *U, double *V, double *W, size_t vo, double u,
+                                          double v, double w) {
+    if (flags & PTV_FLAG_OUT_F32) {
+        reinterpret_cast<float *>(U)[vo] = (float)u;
+        reinterpret_cast<float *>(V)[vo] = (float)v;
+        reinterpret_cast<float *>(W)[vo] = (float)w;
+    } else {
+        U[vo] = u;
+        V[vo] = v;
+        W[vo] = w;
+    }
+}
+
 __device__ __forceinline__ double nan_to_num(double v) {
     if (v != v) return 0.0;
     if (v == INFINITY) return DBL_MAX;
@@ -800,9 +814,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
         return;
     }
     if (!active) {
-        U[vo] = 0.0;
-        V[vo] = 0.0;
-        W[vo] = 0.0;
+        store_out(a.flags, U, V, W, vo, 0.0, 0.0, 0.0);
         return;
     }
 
@@ -823,9 +835,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
         // values[i] of the single nearest particle (k = 1 query), no arithmetic
         const double4 r = pval[max(bp[0], 0)];
         const bool fix = (a.flags & PTV_FLAG_NAN_TO_NUM) != 0;
-        U[vo] = fix ? nan_to_num(r.x) : r.x;
-        V[vo] = fix ? nan_to_num(r.y) : r.y;
-        W[vo] = fix ? nan_to_num(r.z) : r.z;
+        store_out(a.flags, U, V, W, vo, fix ? nan_to_num(r.x) : r.x, fix ? nan_to_num(r.y) : r.y,
+                  fix ? nan_to_num(r.z) : r.z);
         return;
     }
     // k <= 8: the neighbours' value records are all loaded here, before the weight
@@ -908,9 +919,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
 #pragma unroll
         for (int c = 0; c < 3; ++c) out[c] = nan_to_num(out[c]);
     }
-    U[vo] = out[0];
-    V[vo] = out[1];
-    W[vo] = out[2];
+    store_out(a.flags, U, V, W, vo, out[0], out[1], out[2]);
     if constexpr (STAMP) {
         stamp(t_epi);
         const long long gw = (long long)blockIdx.x * 4 + wid;
