@@ -114,6 +114,20 @@ def rank_particles(args, rank, world, values="reference"):
     return np.concatenate(parts), np.concatenate(vals)
 
 
+def row_traffic(*keys):
+    """Sum of HBM bytes per launch of the named row kernels (profiles/traffic_rows_*.json,
+    tools/traffic_rows.py), or None when any is missing."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "traffic_rows_*.json")))
+    if not files:
+        return None
+    try:
+        with open(files[-1]) as f:
+            t = json.load(f)
+        return float(sum(t[k]["hbm_bytes"] for k in keys))
+    except Exception:
+        return None
+
+
 def traffic_from_profiles(kernel_substr="k_knn_interp<"):
     """HBM bytes per k-NN launch from the newest profiles/traffic_*.json (or None)."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "traffic_*.json")))
@@ -279,7 +293,8 @@ def main_div(args):
             "config": {"workload": f"consistent divergence of a {G}^3 {args.div_dtype} field (z-slab per GPU)",
                        "grid": G, "method": "div", "parallelism": f"z-slab x{world}"},
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
+                         "frac": round(ach / HBM_PEAK_GBPS, 4),
+                         "traffic": row_traffic("div:k_divergence") if (G == 512 and not f32) else None,
                          "kernel": f"k_divergence<{'float' if f32 else 'double'}>",
                          "alg_bytes_per_launch": alg, "kernel_ms": round(kavg, 4)},
             "cpu_baseline": cpu,
@@ -393,7 +408,9 @@ def main_filter(args):
                        "particles": n, "method": "filter", "parallelism": f"independent particle sets x{world}"},
             "breakdown_ms": {"bin": round(st["ms_bin"], 3), "knn+stats": round(kavg, 3)},
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
+                         "frac": round(ach / HBM_PEAK_GBPS, 4),
+                         "traffic": row_traffic("filter:k_knn_interp", "filter:k_outlier_stats")
+                         if (k == 25 and n == 5_000_000) else None,
                          "kernel": f"k_knn_interp<{32 if k + 1 <= 32 else 64}> (slot mode) + k_outlier_stats",
                          "alg_bytes_per_launch": alg, "kernel_ms": round(kavg, 4)},
             "cpu_baseline": cpu}), flush=True)
@@ -481,7 +498,9 @@ def main_mask(args):
                        "parallelism": f"independent masks x{world}"},
             "breakdown_ms": {"sample": round(t_s, 4), "boundary": round(t_b, 4)},
             "roofline": {"bound": "hbm", "achieved": round(ach_b, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(ach_b / HBM_PEAK_GBPS, 4), "traffic": None,
+                         "frac": round(ach_b / HBM_PEAK_GBPS, 4),
+                         "traffic": row_traffic("mask:k_boundary_count16", "mask:k_boundary_emit16")
+                         if G == 512 else None,
                          "kernel": "extract_boundary_particles (k_boundary_count + scan + k_boundary_emit)",
                          "alg_bytes_per_launch": alg_b, "kernel_ms": round(t_b, 4),
                          "sample_mask": {"achieved": round(ach_s, 1), "frac": round(ach_s / HBM_PEAK_GBPS, 4),
