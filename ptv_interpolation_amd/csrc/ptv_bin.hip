@@ -77,15 +77,32 @@ __global__ __launch_bounds__(256) void k_bbox(BBoxArgs a, double *partials) {
     if (threadIdx.x < 6) partials[(size_t)blockIdx.x * 6 + threadIdx.x] = red[threadIdx.x][0];
 }
 
-__global__ __launch_bounds__(64) void k_bbox_final(const double *partials, int nblk, double *out) {
-    const int d = threadIdx.x;
-    if (d >= 6) return;
-    double r = d < 3 ? INFINITY : -INFINITY;
-    for (int b = 0; b < nblk; ++b) {
-        double v = partials[(size_t)b * 6 + d];
-        r = d < 3 ? fmin(r, v) : fmax(r, v);
+// 256 threads: strided partial min/max per dimension, then an LDS tree (was 6 serial lanes)
+__global__ __launch_bounds__(256) void k_bbox_final(const double *partials, int nblk, double *out) {
+    double r[6];
+#pragma unroll
+    for (int d = 0; d < 6; ++d) r[d] = d < 3 ? INFINITY : -INFINITY;
+    for (int b = threadIdx.x; b < nblk; b += 256) {
+#pragma unroll
+        for (int d = 0; d < 6; ++d) {
+            const double v = partials[(size_t)b * 6 + d];
+            r[d] = d < 3 ? fmin(r[d], v) : fmax(r[d], v);
+        }
     }
-    out[d] = r;
+    __shared__ double red[6][256];
+#pragma unroll
+    for (int d = 0; d < 6; ++d) red[d][threadIdx.x] = r[d];
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+        if ((int)threadIdx.x < st) {
+#pragma unroll
+            for (int d = 0; d < 6; ++d)
+                red[d][threadIdx.x] = d < 3 ? fmin(red[d][threadIdx.x], red[d][threadIdx.x + st])
+                                            : fmax(red[d][threadIdx.x], red[d][threadIdx.x + st]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < 6) out[threadIdx.x] = red[threadIdx.x][0];
 }
 
 int launch_bbox(const double *const px[3], int64_t n, const double *const qa[3], const int64_t qn[3],
@@ -102,7 +119,7 @@ int launch_bbox(const double *const px[3], int64_t n, const double *const qa[3],
     int nblk = (int)std::min<int64_t>((m + 255) / 256, max_blocks);
     nblk = std::max(nblk, 1);
     hipLaunchKernelGGL(k_bbox, dim3(nblk), dim3(256), 0, s, a, d_partials);
-    hipLaunchKernelGGL(k_bbox_final, dim3(1), dim3(64), 0, s, (const double *)d_partials, nblk, d_out6);
+    hipLaunchKernelGGL(k_bbox_final, dim3(1), dim3(256), 0, s, (const double *)d_partials, nblk, d_out6);
     PTV_HIP(hipGetLastError());
     return PTV_OK;
 }
@@ -255,14 +272,20 @@ __device__ void sift_down(uint32_t *a, int root, int n) {
     }
 }
 
+// sorts each cell's slots by original index and records every particle's final slot
+// (inv[original] = slot) for the placement pass
 __global__ __launch_bounds__(256) void k_seg_sort(const uint32_t *__restrict__ start, size_t m,
-                                                  uint32_t *__restrict__ perm) {
+                                                  uint32_t *__restrict__ perm, uint32_t *__restrict__ inv) {
     size_t c = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= m) return;
     uint32_t s = start[c], e = start[c + 1];
     int n = (int)(e - s);
-    if (n <= 1) return;
+    if (n <= 0) return;
     uint32_t *a = perm + s;
+    if (n == 1) {
+        inv[a[0]] = s;
+        return;
+    }
     if (n <= 48) {
         for (int i = 1; i < n; ++i) {
             uint32_t v = a[i];
@@ -282,16 +305,19 @@ __global__ __launch_bounds__(256) void k_seg_sort(const uint32_t *__restrict__ s
             sift_down(a, 0, end);
         }
     }
+    for (int j = 0; j < n; ++j) inv[a[j]] = s + (uint32_t)j;
 }
 
-__global__ __launch_bounds__(256) void k_gather(const uint32_t *__restrict__ perm, int64_t n,
-                                                const double *__restrict__ x, const double *__restrict__ y,
-                                                const double *__restrict__ z, const double *__restrict__ u,
-                                                const double *__restrict__ v, const double *__restrict__ w,
-                                                double4 *__restrict__ prec, double4 *__restrict__ pval) {
-    int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= n) return;
-    uint32_t i = perm[s];
+// placement in original order: coalesced 48-B reads per particle, two full 32-B record
+// writes at its slot (the slot-order gather read six scattered 8-B values per particle)
+__global__ __launch_bounds__(256) void k_place(const uint32_t *__restrict__ inv, int64_t n,
+                                               const double *__restrict__ x, const double *__restrict__ y,
+                                               const double *__restrict__ z, const double *__restrict__ u,
+                                               const double *__restrict__ v, const double *__restrict__ w,
+                                               double4 *__restrict__ prec, double4 *__restrict__ pval) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t s = inv[i];
     prec[s] = make_double4(x[i], y[i], z[i], (double)i);
     pval[s] = make_double4(u[i], v[i], w[i], 0.0);
 }
@@ -311,9 +337,10 @@ int launch_bin(const CellGrid &cg, const double *const px[3], const double *cons
                        (const uint32_t *)d_scan_partials, sb, d_start);
     hipLaunchKernelGGL(k_scatter, dim3(nb), dim3(256), 0, s, (const uint32_t *)d_code, n,
                        (const uint32_t *)d_start, d_count, d_perm);
+    // d_code is dead after the scatter: it holds the inverse permutation from here on
     hipLaunchKernelGGL(k_seg_sort, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, (const uint32_t *)d_start, m,
-                       d_perm);
-    hipLaunchKernelGGL(k_gather, dim3(nb), dim3(256), 0, s, (const uint32_t *)d_perm, n, px[0], px[1], px[2],
+                       d_perm, d_code);
+    hipLaunchKernelGGL(k_place, dim3(nb), dim3(256), 0, s, (const uint32_t *)d_code, n, px[0], px[1], px[2],
                        pv[0], pv[1], pv[2], d_prec, d_pval);
     PTV_HIP(hipGetLastError());
     return PTV_OK;
