@@ -14,8 +14,6 @@ taken as float64 (the CSV loader's dtype).
 """
 from __future__ import annotations
 
-import os
-
 import numpy as np
 
 from . import _lib
@@ -26,7 +24,9 @@ _MAD_EPS = 1e-6  # filtering.py:46
 
 
 def _device():
-    return int(os.environ.get("PTV_DEVICE", "0"))
+    from . import launcher
+
+    return launcher.devices()[0]
 
 
 def remove_outliers_knn(df, k=25, threshold=3.0):

@@ -28,7 +28,7 @@ import os
 
 import numpy as np
 
-from . import _lib
+from . import _lib, launcher
 
 __all__ = [
     "load_ptv_data",
@@ -189,7 +189,8 @@ def separable_axes(X, Y, Z):
 
 
 def _gpu_device():
-    return int(os.environ.get("PTV_DEVICE", "0"))
+    """The device of single-device calls (mask path): PTV_DEVICE, else the first of launcher.devices()."""
+    return launcher.devices()[0]
 
 
 def _knn_field(points, values, grid_tuple, method, k, power):
@@ -207,12 +208,14 @@ def _knn_field(points, values, grid_tuple, method, k, power):
     if k > n:
         # KDTree pads missing neighbours with index n; values[indices] then fails
         raise IndexError(f"index {n} is out of bounds for axis 0 with size {n}")
-    ctx = _lib.Context.get(_gpu_device())
     m = {"idw": _lib.METHOD_IDW, "sibson": _lib.METHOD_SIBSON, "nearest": _lib.METHOD_NEAREST}[method]
     axes = separable_axes(X, Y, Z)
     if axes is not None:
-        U, V, W = ctx.interp_knn(points, values, axes=axes, method=m, k=k, power=power, eps=_EPS)
+        # z-slab per device (launcher.py); bit-identical to one whole-grid call
+        U, V, W = launcher.run_slabs(len(axes[2]), lambda ctx, z0, z1: ctx.interp_knn(
+            points, values, axes=axes, method=m, k=k, power=power, eps=_EPS, z_range=(z0, z1)))
     else:
+        ctx = _lib.Context.get(launcher.devices()[0])
         size = int(np.prod(shape))
         g = [np.ascontiguousarray(np.asarray(A, dtype=np.float64)).reshape(-1) for A in (X, Y, Z)]
         sh = tuple(shape) if len(shape) == 3 else (1, 1, size)

@@ -35,9 +35,9 @@ MAX_SYSTEM = 64  # include/ptv_api.h: k + C(degree + 3, 3) <= 64
 
 
 def _device():
-    import os
+    from . import launcher
 
-    return int(os.environ.get("PTV_DEVICE", "0"))
+    return launcher.devices()[0]
 
 
 class LocalRBFInterpolator:
@@ -123,8 +123,8 @@ class LocalRBFInterpolator:
             g[:, : min(3, S - c0)] = self.d[:, c0:c0 + 3]
             yield c0, min(3, S - c0), g
 
-    def _run(self, **grid):
-        ctx = _lib.Context.get(_device())
+    def _run(self, ctx=None, **grid):
+        ctx = ctx if ctx is not None else _lib.Context.get(_device())
         outs = []
         for c0, w, g in self._groups():
             res = ctx.interp_rbf(self.y, g, k=self.neighbors, kernel=self.kernel, epsilon=self.epsilon,
@@ -147,10 +147,10 @@ class LocalRBFInterpolator:
         out = np.stack([c.reshape(-1) for c in comps], axis=-1)
         return out.reshape((nx,) + self.d_shape)
 
-    def evaluate_grid(self, ax, ay, az, fluid_mask=None, flags=0, z_range=None):
+    def evaluate_grid(self, ax, ay, az, fluid_mask=None, flags=0, z_range=None, ctx=None):
         """Evaluate on the separable grid meshgrid(az, ay, ax, 'ij') (create_grid axes) without
         materialising the (V, 3) query list; returns one (nz', ny, nx) array per component."""
-        return self._run(axes=(ax, ay, az), fluid_mask=fluid_mask, flags=flags, z_range=z_range)
+        return self._run(ctx=ctx, axes=(ax, ay, az), fluid_mask=fluid_mask, flags=flags, z_range=z_range)
 
 
 def rbf_field(points, values, grid_tuple, k, kernel, smoothing, n_jobs=1):
@@ -171,7 +171,11 @@ def rbf_field(points, values, grid_tuple, k, kernel, smoothing, n_jobs=1):
         print(f"Interpolating {n_points} points serially...")
     axes = separable_axes(X, Y, Z)
     if axes is not None:
-        U, V, W = interp.evaluate_grid(*axes)
+        from . import launcher
+
+        # z-slab per device (launcher.py), as interpolator.py:173-182 fans out over processes
+        U, V, W = launcher.run_slabs(len(axes[2]), lambda ctx, z0, z1: tuple(
+            interp.evaluate_grid(*axes, z_range=(z0, z1), ctx=ctx)))
     else:
         flat = np.stack([np.ravel(X), np.ravel(Y), np.ravel(Z)], axis=-1)
         out = interp(flat)

@@ -1,0 +1,36 @@
+"""Multi-device z-slab launcher of the drop-in API (ptv_interpolation_amd/launcher.py,
+SURVEY §8(e)): slabs on several contexts reproduce the single-call result bit for bit.
+On a one-GPU box the devices are repeated (PTV_DEVICES=0,0,0: three contexts, three
+streams, three host threads on the same GPU)."""
+import contextlib
+import io
+
+import numpy as np
+import pandas as pd
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _df(P, Q):
+    return pd.DataFrame({"x": P[:, 0], "y": P[:, 1], "z": P[:, 2], "u": Q[:, 0], "v": Q[:, 1], "w": Q[:, 2]})
+
+
+@pytest.mark.parametrize("method,kw", [("idw", {"idw_neighbors": 8}), ("idw", {"idw_neighbors": 50}),
+                                       ("sibson", {"sibson_neighbors": 30}), ("nearest", {}),
+                                       ("rbf", {"rbf_neighbors": 20})])
+def test_slabs_on_three_contexts_equal_one_call(monkeypatch, method, kw):
+    from ptv_interpolation_amd import interpolator as ip
+    from ptv_interpolation_amd import synth
+
+    G = 40 if method == "rbf" else 64
+    P, Q = synth.sphere_pack(20000 if method != "rbf" else 6000, G, values="normal")
+    (X, Y, Z), _ = ip.create_grid(((0, G),) * 3, (G, G, 37))  # 37 planes: uneven slabs
+    with contextlib.redirect_stdout(io.StringIO()):
+        monkeypatch.setenv("PTV_DEVICE", "0")
+        one = ip.interpolate_field(_df(P, Q), (X, Y, Z), method=method, **kw)
+        monkeypatch.delenv("PTV_DEVICE")
+        monkeypatch.setenv("PTV_DEVICES", "0,0,0")
+        three = ip.interpolate_field(_df(P, Q), (X, Y, Z), method=method, **kw)
+    for a, b in zip(three, one):
+        assert a.shape == X.shape and np.array_equal(a, b, equal_nan=True)

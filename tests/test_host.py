@@ -148,3 +148,15 @@ def test_divergence_host_rules_before_any_gpu_call():
     assert physics._result_dtype(np.dtype(np.float64), np.float32(0.5)) == np.float64
     x = np.linspace(0, 9, 10)
     assert physics._result_dtype(f32, x[1] - x[0]) == np.float64  # view_divergence.py:22
+
+
+def test_launcher_slabs_and_device_list(monkeypatch):
+    from ptv_interpolation_amd import launcher
+
+    assert launcher.slab_bounds(10, 3) == [(0, 3), (3, 6), (6, 10)]
+    assert launcher.slab_bounds(2, 8) == [(0, 1), (1, 2)]
+    assert launcher.slab_bounds(512, 8)[-1] == (448, 512)
+    monkeypatch.setenv("PTV_DEVICES", "0, 2,3")
+    assert launcher.devices() == [0, 2, 3]
+    monkeypatch.setenv("PTV_DEVICE", "5")
+    assert launcher.devices() == [5]
