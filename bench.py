@@ -87,6 +87,9 @@ def parse():
     ap.add_argument("--out-dtype", default="f64", choices=["f64", "f32"],
                     help="k-NN methods: U, V, W stored as float32 (PTV_FLAG_OUT_F32, the fused main.py:230 "
                          "astype; arithmetic stays f64) — the C5 configuration's field")
+    ap.add_argument("--mask", action="store_true",
+                    help="k-NN methods: sphere-pack fluid mask + NaN fill fused (main.py:195-207; the C4 masked "
+                         "geometry): solid voxels are skipped and written as 0")
     ap.add_argument("--halo", type=int, default=64, help="neighbour-copy halo (voxels) for N>1")
     ap.add_argument("--cpu-sample-planes", type=int, default=16)
     ap.add_argument("--cpu-workers", type=int, default=16)
@@ -547,6 +550,14 @@ def main():
            [torch.from_numpy(np.ascontiguousarray(Q[:, i])).to(dev) for i in range(3)]
     axes = [torch.from_numpy(ax_h).to(dev), torch.from_numpy(ax_h.copy()).to(dev), torch.from_numpy(az_h).to(dev)]
     out_f32 = args.out_dtype == "f32" and args.method != "rbf"
+    mask_t = None
+    if args.mask:
+        from ptv_interpolation_amd import synth as _synth
+
+        fm = _synth.fluid_mask(G)
+        fluid_frac = float(fm.mean())
+        mask_t = torch.from_numpy(np.ascontiguousarray(fm).view(np.uint8)).to(dev)
+        del fm
     out = [torch.empty((G, G, G), dtype=torch.float32 if out_f32 else torch.float64, device=dev) for _ in range(3)]
     ctx = _lib.Context(local)
     method = {"idw": _lib.METHOD_IDW, "sibson": _lib.METHOD_SIBSON, "nearest": _lib.METHOD_NEAREST}.get(args.method)
@@ -568,7 +579,9 @@ def main():
                                       axes_ptrs=[a.data_ptr() for a in axes],
                                       out_ptrs=[o.data_ptr() for o in out], method=method, k=args.k,
                                       power=args.power, stream=stream,
-                                      flags=_lib.FLAG_OUT_F32 if out_f32 else 0)
+                                      mask_ptr=mask_t.data_ptr() if mask_t is not None else 0,
+                                      flags=(_lib.FLAG_OUT_F32 if out_f32 else 0) |
+                                            (_lib.FLAG_NAN_TO_NUM if mask_t is not None else 0))
 
     for _ in range(args.warmup):
         step()
@@ -612,6 +625,8 @@ def main():
     value = vox * world / (elapsed / args.steps) / 1e6
     knn_avg = float(np.mean(knn_ms))
     alg_bytes = vox * ((6 * args.k) * 8 + 3 * (4 if out_f32 else 8))
+    if args.mask:  # solid voxels are skipped, fluid V in the gather term; + the mask bytes
+        alg_bytes = int(round(vox * fluid_frac)) * (6 * args.k) * 8 + vox * (3 * (4 if out_f32 else 8) + 1)
     achieved = alg_bytes / (knn_avg * 1e-3) / 1e9
     traffic = traffic_from_profiles()
 
@@ -654,12 +669,14 @@ def main():
                        if args.method == "rbf" else
                        f"{G}^3 grid / {args.particles} particles {args.method.upper()} "
                        f"k={args.k} p={args.power} fp64" + (" (float32 U, V, W)" if out_f32 else "") +
+                       (f" + sphere-pack fluid mask ({fluid_frac:.1%} fluid, solid skipped)" if args.mask else "") +
                        " (z-slab per GPU)",
                        "grid": G, "particles": args.particles, "particles_binned_rank0": n,
                        "method": args.method, "k": args.k, "power": args.power,
                        "parallelism": f"z-slab x{world}"},
             "roofline": roof,
             "cpu_baseline": cpu,
+            **({"fluid_mvoxels_per_s": round(value * fluid_frac, 2)} if args.mask else {}),
             "breakdown_ms": {"bin": round(float(np.mean(bin_ms)), 3), "lattice": round(float(np.mean(lat_ms)), 3),
                              "knn": round(knn_avg, 3), "solve": round(float(np.mean(solve_ms)), 3)},
         }
