@@ -214,10 +214,10 @@ __device__ __forceinline__ void build_entries(double *__restrict__ sc, int lane,
     }
 }
 
-constexpr int kBuildCols = 16;  // system columns built per LDS round
+constexpr int kBuildCols = 8;  // system columns built per LDS round (8: 44 KB of LDS per block, 3 blocks per CU)
 
 template <int M, int L>
-__global__ __launch_bounds__(256) void k_rbf_local(RbfKernelArgs a, const double4 *__restrict__ prec,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M <= 32 ? 3 : 1))) void k_rbf_local(RbfKernelArgs a, const double4 *__restrict__ prec,
                                                    const double4 *__restrict__ pval,
                                                    const uint32_t *__restrict__ slots,
                                                    const double *__restrict__ ax, const double *__restrict__ ay,
