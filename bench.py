@@ -90,6 +90,7 @@ def parse():
     ap.add_argument("--mask", action="store_true",
                     help="k-NN methods: sphere-pack fluid mask + NaN fill fused (main.py:195-207; the C4 masked "
                          "geometry): solid voxels are skipped and written as 0")
+    ap.add_argument("--r0-scale", type=float, default=0.0, help="dev: first search radius / expected k-NN radius")
     ap.add_argument("--halo", type=int, default=64, help="neighbour-copy halo (voxels) for N>1")
     ap.add_argument("--cpu-sample-planes", type=int, default=16)
     ap.add_argument("--cpu-workers", type=int, default=16)
@@ -133,7 +134,10 @@ def row_traffic(*keys):
 
 def traffic_from_profiles(kernel_substr="k_knn_interp<"):
     """HBM bytes per k-NN launch from the newest profiles/traffic_*.json (or None)."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "traffic_*.json")))
+    import re
+
+    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "traffic_r*.json"))
+                   if re.fullmatch(r"traffic_r\d+\.json", os.path.basename(f)))  # not traffic_rows_*
     if not files:
         return None
     try:
@@ -580,6 +584,7 @@ def main():
                                       out_ptrs=[o.data_ptr() for o in out], method=method, k=args.k,
                                       power=args.power, stream=stream,
                                       mask_ptr=mask_t.data_ptr() if mask_t is not None else 0,
+                                      r0_scale=args.r0_scale,
                                       flags=(_lib.FLAG_OUT_F32 if out_f32 else 0) |
                                             (_lib.FLAG_NAN_TO_NUM if mask_t is not None else 0))
 

@@ -17,4 +17,8 @@ timeout -k 10 300 python -u bench.py --method nearest --steps 5 --warmup 2 > gpu
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_${R}_div; rm -rf "$OUT"; mkdir -p "$OUT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -- python3 bench.py --method div --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/stats.log" 2>&1 || exit 1
+timeout -k 10 400 python -u bench.py --method rbf --k 32 --rbf-kernel gaussian --epsilon 0.3 --degree -1 --steps 2 --warmup 1 > gpurun_out/${R}_rbf_gaussian_bench.json 2> gpurun_out/${R}_rbf.err || { tail -20 gpurun_out/${R}_rbf.err; exit 1; }
+timeout -k 10 300 python -u bench.py --method filter --steps 5 --warmup 2 > gpurun_out/${R}_filter_bench.json 2> gpurun_out/${R}_filter.err || { tail -20 gpurun_out/${R}_filter.err; exit 1; }
+timeout -k 10 300 python -u bench.py --method mask --steps 10 --warmup 3 > gpurun_out/${R}_mask_bench.json 2> gpurun_out/${R}_mask.err || { tail -20 gpurun_out/${R}_mask.err; exit 1; }
+timeout -k 10 300 python -u bench.py --mask --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/${R}_masked512_bench.json 2> gpurun_out/${R}_m512.err || { tail -20 gpurun_out/${R}_m512.err; exit 1; }
 cat gpurun_out/${R}_bench.json
