@@ -79,8 +79,7 @@ struct ptv_ctx {
     DevBuf<unsigned long long> bnd_counts;                       // boundary: per-block counts / offsets
     DevBuf<double> bnd_xyz;                                      // boundary host calls: coordinates
     DevBuf<uint8_t> flt_keep;                                    // outlier filter host calls
-    DevBuf<uint32_t> flt_code, flt_perm, flt_count, flt_start, flt_scanp;  // filter: query bricks
-    DevBuf<double4> flt_prec, flt_pval;
+    DevBuf<uint32_t> flt_code, flt_perm, flt_count, flt_start, flt_scanp;  // filter: Morton keys/ids, sort temp
     DevBuf<double> flt_kth;
     hipEvent_t ev_div0 = nullptr, ev_div1 = nullptr;             // around the divergence stencil
     bool div_pending = false;
@@ -194,8 +193,6 @@ int ptv_free(ptv_ctx *c) {
     c->bnd_xyz.release();
     c->flt_keep.release();
     for (auto *b : {&c->flt_code, &c->flt_perm, &c->flt_count, &c->flt_start, &c->flt_scanp}) b->release();
-    c->flt_prec.release();
-    c->flt_pval.release();
     c->flt_kth.release();
     hipEventDestroy(c->ev_div0);
     hipEventDestroy(c->ev_div1);
@@ -1199,43 +1196,39 @@ int filter_check(ptv_ctx *c, const ptv_particles *p, const ptv_filter_params *pr
 int run_filter(ptv_ctx *c, const ptv_particles *p, const ptv_filter_params *prm, uint8_t *keep, double *kth,
                hipStream_t s) {
     const int64_t n = p->n;
-    const int64_t npad = (n + 63) & ~(int64_t)63;  // 64 queries per wave tile (4 x 4 x 4)
+    const int64_t npad = (n + 255) & ~(int64_t)255;  // 64 queries per wave tile, 4 tiles per block
     for (int i = 0; i < 3; ++i) PTV_TRY(c->qpts[i].ensure(npad));
     PTV_TRY(launch_pad_queries(p->x, p->y, p->z, n, npad, c->qpts[0].p, c->qpts[1].p, c->qpts[2].p, s));
     ptv_grid g{};
-    g.nx = 4;
+    g.nx = 16;  // 4 wave tiles along x per block (ptv_filter.hip pos_of)
     g.ny = 4;
-    g.nz = npad / 16;
+    g.nz = npad / 64;
     g.px = c->qpts[0].p;
     g.py = c->qpts[1].p;
     g.pz = c->qpts[2].p;
     g.z_begin = 0;
     g.z_end = g.nz;
-    double r0s = 0.0, occ = 0.0, brick = 32.0;  // brick 32: 87.5 ms vs 92.4 at 64 (5M, k = 25)
+    double r0s = 0.0, occ = 0.0;
     if (const char *e = std::getenv("PTV_FILTER_R0")) r0s = std::atof(e);       // dev knobs
     if (const char *e = std::getenv("PTV_FILTER_OCC")) occ = std::atof(e);
-    if (const char *e = std::getenv("PTV_FILTER_BRICK")) brick = std::atof(e);
     const SearchParams sp{PTV_METHOD_IDW, prm->k + 1, 2.0, 1e-10, 0u, occ, r0s, -1};
     KnnLaunch kl;
     Binned b{};
     PTV_TRY(prepare(c, p, &g, &sp, nullptr, nullptr, nullptr, g.px, g.py, g.pz, s, kl, b));
-    // query order: a counting sort into bricks of ~32 particles (a wave's queries are one
-    // compact blob), over the bounding box prepare() measured
+    // query order: Morton order of the particles over the bounding box prepare() measured,
+    // laid out in the k-NN kernel's sub-ball lane pattern (ptv_filter.hip)
     const double lo[3] = {c->h_bbox[0], c->h_bbox[1], c->h_bbox[2]};
     const double hi[3] = {c->h_bbox[3], c->h_bbox[4], c->h_bbox[5]};
-    const CellGrid qg = make_cell_grid(lo, hi, n, brick);
-    const size_t qm = (size_t)qg.ncells;
+    const size_t tb = morton_sort_temp_bytes(n);
     PTV_TRY(c->flt_code.ensure(n));
+    PTV_TRY(c->flt_count.ensure(n));
+    PTV_TRY(c->flt_start.ensure(n));
     PTV_TRY(c->flt_perm.ensure(n));
-    PTV_TRY(c->flt_prec.ensure(n));
-    PTV_TRY(c->flt_pval.ensure(n));
-    PTV_TRY(c->flt_count.ensure(qm));
-    PTV_TRY(c->flt_start.ensure(qm + 1));
-    PTV_TRY(c->flt_scanp.ensure(scan_partials_needed(qm) + 1));
-    const double *pp[3] = {p->x, p->y, p->z}, *pv[3] = {p->u, p->v, p->w};
-    PTV_TRY(launch_bin(qg, pp, pv, n, c->flt_code.p, c->flt_perm.p, c->flt_count.p, c->flt_start.p, c->flt_scanp.p,
-                       c->flt_prec.p, c->flt_pval.p, s));
-    PTV_TRY(launch_binned_queries(c->flt_prec.p, n, npad, c->qpts[0].p, c->qpts[1].p, c->qpts[2].p, s));
+    PTV_TRY(c->flt_scanp.ensure(tb / 4 + 1));
+    PTV_TRY(launch_morton_order(p->x, p->y, p->z, n, lo, hi, c->flt_code.p, c->flt_count.p, c->flt_start.p,
+                                c->flt_perm.p, c->flt_scanp.p, tb, s));
+    PTV_TRY(launch_query_layout(c->flt_perm.p, p->x, p->y, p->z, n, npad, c->qpts[0].p, c->qpts[1].p, c->qpts[2].p,
+                                s));
     PTV_TRY(c->slots.ensure((size_t)npad * (prm->k + 1)));
     kl.mode = kModeSlots;
     kl.slots = c->slots.p;
@@ -1243,7 +1236,8 @@ int run_filter(ptv_ctx *c, const ptv_particles *p, const ptv_filter_params *prm,
     PTV_TRY(launch_knn(kl, b, nullptr, nullptr, nullptr, c->qpts[0].p, c->qpts[1].p, c->qpts[2].p, nullptr, nullptr,
                        nullptr, nullptr, s));
     FilterArgs fa{n, prm->k, prm->threshold, prm->mad_eps};
-    PTV_TRY(launch_outlier_stats(fa, b, c->flt_prec.p, c->flt_pval.p, c->slots.p, keep, kth, s));
+    const ParticleCols pc{p->x, p->y, p->z, p->u, p->v, p->w};
+    PTV_TRY(launch_outlier_stats(fa, b, c->flt_perm.p, pc, c->slots.p, keep, kth, s));
     PTV_HIP(hipEventRecord(c->ev_knn1, s));
     c->timed_pending = true;
     c->last.n_voxels = n;

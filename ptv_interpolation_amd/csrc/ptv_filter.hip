@@ -8,17 +8,22 @@
 //   keep = |speed - med| / (mad + 1e-6) <= threshold                   (:47-51)
 //
 // The (k+1)-NN query runs on the same k-NN kernel as the grid path (slot mode, the
-// particles themselves as a point-list "grid").  The query order is a second counting
-// sort of the particles into coarse bricks of ~64 particles, so that a wave's 64 queries
-// form a compact blob (the search-cell order would make them a thin strip along x, whose
-// gather box is ~10x larger).  This file holds the two thin kernels either side of the
-// search: building the query list, and the per-particle statistics.
+// particles themselves as a point-list "grid").  Query order: the particles sorted by a
+// 30-bit Morton code (hipCUB radix sort, stable: ties keep index order), so that 64
+// consecutive queries are a compact blob and 8 consecutive ones a compact sub-blob.  Each
+// wave tile of 64 is then laid out like a 4x4x4 voxel tile: the 8 queries of Morton
+// sub-group s go to the lanes whose bits (1, 3, 5) spell s, which is how the k-NN kernel
+// groups lanes into its 8 sub-balls (ptv_knn.hip), so the sub-ball candidate filter
+// works on particle queries too.  This file holds the kernels either side of the search:
+// the Morton sort and query layout, and the per-particle statistics.
+#include <hipcub/hipcub.hpp>
+
 #include "ptv_api.h"
 #include "ptv_kernels.hpp"
 
 namespace ptv {
 
-// queries in brick order, padded to `npad` with the last record
+// queries in record order, padded to `npad` with the last record
 __global__ __launch_bounds__(256) void k_binned_queries(const double4 *__restrict__ prec, int64_t n, int64_t npad,
                                                         double *__restrict__ qx, double *__restrict__ qy,
                                                         double *__restrict__ qz) {
@@ -41,6 +46,66 @@ __global__ __launch_bounds__(256) void k_pad_queries(const double *__restrict__ 
     qx[i] = x[j];
     qy[i] = y[j];
     qz[i] = z[j];
+}
+
+__device__ __forceinline__ uint32_t spread10(uint32_t v) {  // 10 bits -> every third bit
+    v &= 0x3ffu;
+    v = (v | (v << 16)) & 0x030000ffu;
+    v = (v | (v << 8)) & 0x0300f00fu;
+    v = (v | (v << 4)) & 0x030c30c3u;
+    v = (v | (v << 2)) & 0x09249249u;
+    return v;
+}
+
+__global__ __launch_bounds__(256) void k_morton(const double *__restrict__ x, const double *__restrict__ y,
+                                                const double *__restrict__ z, int64_t n, double ox, double oy,
+                                                double oz, double sx, double sy, double sz,
+                                                uint32_t *__restrict__ keys, uint32_t *__restrict__ ids) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    auto q = [](double v, double o, double sc) {
+        const double f = (v - o) * sc;
+        return (uint32_t)(f < 0.0 ? 0.0 : (f > 1023.0 ? 1023.0 : f));
+    };
+    keys[i] = spread10(q(x[i], ox, sx)) | (spread10(q(y[i], oy, sy)) << 1) | (spread10(q(z[i], oz, sz)) << 2);
+    ids[i] = (uint32_t)i;
+}
+
+// query q of a 64-tile (Morton rank within the tile) <-> lane: sub-group s = q >> 3 sits on
+// lane bits (1, 3, 5), member j = q & 7 on bits (0, 2, 4)
+__device__ __forceinline__ int lane_of_query(int q) {
+    const int s = q >> 3, j = q & 7;
+    return (j & 1) | ((s & 1) << 1) | (((j >> 1) & 1) << 2) | (((s >> 1) & 1) << 3) | (((j >> 2) & 1) << 4) |
+           (((s >> 2) & 1) << 5);
+}
+__device__ __forceinline__ int query_of_lane(int l) {
+    const int s = ((l >> 1) & 1) | (((l >> 3) & 1) << 1) | (((l >> 5) & 1) << 2);
+    const int j = (l & 1) | (((l >> 2) & 1) << 1) | (((l >> 4) & 1) << 2);
+    return (s << 3) | j;
+}
+
+// Point-list "grid" of the search: nx = 16, ny = 4, nz = npad / 64, so a 256-thread block
+// holds 4 wave tiles along x (all four waves busy; with nx = 4 three of them idled).  Tile
+// g = 4 tz + tx covers lanes l at ((4 tz + l / 16) * 4 + (l / 4) % 4) * 16 + 4 tx + l % 4.
+__device__ __forceinline__ int64_t pos_of(int64_t g, int l) {
+    const int64_t tz = g >> 2, tx = g & 3;
+    return ((tz * 4 + (l >> 4)) * 4 + ((l >> 2) & 3)) * 16 + tx * 4 + (l & 3);
+}
+
+// position of tile g / lane l holds Morton query 64 g + query_of_lane(l) (the last particle
+// pads the final tiles)
+__global__ __launch_bounds__(256) void k_query_layout(const uint32_t *__restrict__ perm, const double *__restrict__ x,
+                                                      const double *__restrict__ y, const double *__restrict__ z,
+                                                      int64_t n, int64_t npad, double *__restrict__ qx,
+                                                      double *__restrict__ qy, double *__restrict__ qz) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (tile, lane) = (t / 64, t % 64)
+    if (t >= npad) return;
+    const int64_t q = (t & ~(int64_t)63) + query_of_lane((int)(t & 63));
+    const uint32_t src = perm[q < n ? q : n - 1];
+    const int64_t p = pos_of(t >> 6, (int)(t & 63));
+    qx[p] = x[src];
+    qy[p] = y[src];
+    qz[p] = z[src];
 }
 
 // value at sorted position `pos` of s[0..n): the element whose [#less, #less-or-equal) holds pos
@@ -87,15 +152,16 @@ __device__ __forceinline__ double speed_of(const double4 v) {
 template <int KMAX>
 __global__ __launch_bounds__(256) void k_outlier_stats(FilterArgs a, const double4 *__restrict__ prec,
                                                        const double4 *__restrict__ pval,
-                                                       const double4 *__restrict__ qrec,
-                                                       const double4 *__restrict__ qval,
+                                                       const uint32_t *__restrict__ perm, ParticleCols pc,
                                                        const uint32_t *__restrict__ slots, uint8_t *__restrict__ keep,
                                                        double *__restrict__ kth) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // Morton rank of the query
     if (i >= a.n) return;
     const int k1 = a.k + 1;
-    const double4 q = qrec[i];  // query i (brick order); .w = original index
-    const uint32_t *sl = slots + (size_t)i * k1;
+    const uint32_t orig = perm[i];
+    const double4 q = make_double4(pc.x[orig], pc.y[orig], pc.z[orig], (double)orig);
+    const int64_t pos = pos_of(i >> 6, lane_of_query((int)(i & 63)));
+    const uint32_t *sl = slots + (size_t)pos * k1;
     // the point itself is column 0 of the reference query (distance 0); when several
     // particles coincide with it, the query point's own record is the one dropped
     int drop = -1;
@@ -136,8 +202,7 @@ __global__ __launch_bounds__(256) void k_outlier_stats(FilterArgs a, const doubl
 #pragma unroll
     for (int t = 0; t < KMAX; ++t) dev[t] = fabs(sp[t] - med);
     const double mad = median_of(dev, a.k);
-    const double z = fabs(speed_of(qval[i]) - med) / (mad + a.mad_eps);
-    const int64_t orig = (int64_t)q.w;
+    const double z = fabs(speed_of(make_double4(pc.u[orig], pc.v[orig], pc.w[orig], 0.0)) - med) / (mad + a.mad_eps);
     keep[orig] = z <= a.threshold ? 1 : 0;
     if (kth) kth[orig] = dmax;
 }
@@ -166,14 +231,46 @@ int launch_pad_queries(const double *x, const double *y, const double *z, int64_
     return PTV_OK;
 }
 
-int launch_outlier_stats(const FilterArgs &a, const Binned &b, const double4 *qrec, const double4 *qval,
+size_t morton_sort_temp_bytes(int64_t n) {
+    size_t bytes = 0;
+    hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                       (const uint32_t *)nullptr, (uint32_t *)nullptr, (int)n, 0, 30, nullptr);
+    return bytes;
+}
+
+int launch_morton_order(const double *x, const double *y, const double *z, int64_t n, const double lo[3],
+                        const double hi[3], uint32_t *keys, uint32_t *keys_out, uint32_t *ids, uint32_t *perm,
+                        void *temp, size_t temp_bytes, hipStream_t s) {
+    double sc[3];
+    for (int d = 0; d < 3; ++d) {
+        const double e = hi[d] - lo[d];
+        sc[d] = e > 0.0 ? 1024.0 / e : 0.0;
+    }
+    hipLaunchKernelGGL(k_morton, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, y, z, n, lo[0], lo[1], lo[2],
+                       sc[0], sc[1], sc[2], keys, ids);
+    size_t bytes = temp_bytes;
+    PTV_HIP(hipcub::DeviceRadixSort::SortPairs(temp, bytes, (const uint32_t *)keys, keys_out, (const uint32_t *)ids,
+                                               perm, (int)n, 0, 30, s));
+    PTV_HIP(hipGetLastError());
+    return PTV_OK;
+}
+
+int launch_query_layout(const uint32_t *perm, const double *x, const double *y, const double *z, int64_t n,
+                        int64_t npad, double *qx, double *qy, double *qz, hipStream_t s) {
+    hipLaunchKernelGGL(k_query_layout, dim3((unsigned)((npad + 255) / 256)), dim3(256), 0, s, perm, x, y, z, n, npad,
+                       qx, qy, qz);
+    PTV_HIP(hipGetLastError());
+    return PTV_OK;
+}
+
+int launch_outlier_stats(const FilterArgs &a, const Binned &b, const uint32_t *perm, const ParticleCols &pc,
                          const uint32_t *slots, uint8_t *keep, double *kth, hipStream_t s) {
     const dim3 grid((unsigned)((a.n + 255) / 256));
     switch (filter_kmax(a.k)) {
-        case 8: hipLaunchKernelGGL(k_outlier_stats<8>, grid, dim3(256), 0, s, a, b.prec, b.pval, qrec, qval, slots, keep, kth); break;
-        case 16: hipLaunchKernelGGL(k_outlier_stats<16>, grid, dim3(256), 0, s, a, b.prec, b.pval, qrec, qval, slots, keep, kth); break;
-        case 32: hipLaunchKernelGGL(k_outlier_stats<32>, grid, dim3(256), 0, s, a, b.prec, b.pval, qrec, qval, slots, keep, kth); break;
-        case 64: hipLaunchKernelGGL(k_outlier_stats<64>, grid, dim3(256), 0, s, a, b.prec, b.pval, qrec, qval, slots, keep, kth); break;
+        case 8: hipLaunchKernelGGL(k_outlier_stats<8>, grid, dim3(256), 0, s, a, b.prec, b.pval, perm, pc, slots, keep, kth); break;
+        case 16: hipLaunchKernelGGL(k_outlier_stats<16>, grid, dim3(256), 0, s, a, b.prec, b.pval, perm, pc, slots, keep, kth); break;
+        case 32: hipLaunchKernelGGL(k_outlier_stats<32>, grid, dim3(256), 0, s, a, b.prec, b.pval, perm, pc, slots, keep, kth); break;
+        case 64: hipLaunchKernelGGL(k_outlier_stats<64>, grid, dim3(256), 0, s, a, b.prec, b.pval, perm, pc, slots, keep, kth); break;
         default:
             set_error("outlier filter: k must be <= 63 (k + 1 neighbours on the GPU k-NN list)");
             return PTV_E_UNSUPPORTED;

@@ -152,8 +152,19 @@ int launch_pad_queries(const double *x, const double *y, const double *z, int64_
                        double *qy, double *qz, hipStream_t s);
 int launch_binned_queries(const double4 *prec, int64_t n, int64_t npad, double *qx, double *qy, double *qz,
                           hipStream_t s);
-// qrec/qval: the query particles (records {x,y,z,original index}, values) in query order
-int launch_outlier_stats(const FilterArgs &a, const Binned &b, const double4 *qrec, const double4 *qval,
+struct ParticleCols {
+    const double *x, *y, *z, *u, *v, *w;  // original order
+};
+size_t morton_sort_temp_bytes(int64_t n);
+// perm = particle indices sorted by a 30-bit Morton code over [lo, hi] (stable)
+int launch_morton_order(const double *x, const double *y, const double *z, int64_t n, const double lo[3],
+                        const double hi[3], uint32_t *keys, uint32_t *keys_out, uint32_t *ids, uint32_t *perm,
+                        void *temp, size_t temp_bytes, hipStream_t s);
+// point-list query arrays (npad) in the sub-ball lane layout of the Morton order
+int launch_query_layout(const uint32_t *perm, const double *x, const double *y, const double *z, int64_t n,
+                        int64_t npad, double *qx, double *qy, double *qz, hipStream_t s);
+// perm: Morton order of the queries; slots at the laid-out positions
+int launch_outlier_stats(const FilterArgs &a, const Binned &b, const uint32_t *perm, const ParticleCols &pc,
                          const uint32_t *slots, uint8_t *keep, double *kth, hipStream_t s);
 
 }  // namespace ptv

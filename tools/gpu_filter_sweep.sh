@@ -1,5 +1,5 @@
 #!/bin/bash
-# Dev sweep of the outlier-filter search knobs (first radius scale, cell occupancy, query brick size).
+# Dev sweep of the outlier-filter search knobs (first radius scale, cell occupancy).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 mkdir -p gpurun_out
@@ -9,11 +9,7 @@ run() {
 }
 run PTV_FILTER_R0=1.0
 run PTV_FILTER_R0=1.3
-run PTV_FILTER_R0=1.6
-run PTV_FILTER_R0=2.0
+run PTV_FILTER_R0=0.8
 run PTV_FILTER_OCC=0.6
 run PTV_FILTER_OCC=2.5
 run PTV_FILTER_OCC=5.5
-run PTV_FILTER_BRICK=32
-run PTV_FILTER_BRICK=128
-run PTV_FILTER_BRICK=16
