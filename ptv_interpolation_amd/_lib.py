@@ -214,6 +214,24 @@ def dev_dp(ptr: int):
     return C.cast(C.c_void_p(ptr), _dp)
 
 
+def _flat_tiles(gp, shape, fluid_mask, z_range):
+    """A flat point list (shape (1, 1, n)) as a (npad / 64, 4, 16) point grid, padded with
+    the last point: the k-NN kernels tile 4 x 4 x 4 (x, y, z) blocks of the shape, so a
+    (1, 1, n) list would keep only 4 of a wave's 64 lanes busy.  Every query is independent,
+    so the results are the same; returns (gp, shape, mask, unpad) or None."""
+    nz, ny, nx = shape
+    if nz != 1 or ny != 1 or z_range is not None or nx < 64:
+        return None
+    n = nx
+    npad = (n + 255) // 256 * 256
+    ext = [np.concatenate([a, np.full(npad - n, a[-1])]) if npad > n else a for a in gp]
+    mk = None
+    if fluid_mask is not None:
+        m = np.ascontiguousarray(fluid_mask, dtype=np.uint8).ravel()
+        mk = np.concatenate([m, np.zeros(npad - n, dtype=np.uint8)]) if npad > n else m
+    return ext, (npad // 64, 4, 16), mk, (lambda a: a.reshape(-1)[:n].reshape(shape))
+
+
 class Context:
     """One device context (stream + reusable device buffers)."""
 
@@ -363,8 +381,16 @@ class Context:
             keep += [ax, ay, az]
             G = Grid(nx, ny, nz, as_dp(ax), as_dp(ay), as_dp(az), None, None, None, 0, nz)
         else:
-            nz, ny, nx = shape
             gp = [np.ascontiguousarray(a, dtype=np.float64).ravel() for a in grid_points]
+            ft = _flat_tiles(gp, shape, fluid_mask, z_range)
+            if ft is not None:
+                gp, tshape, fm, unpad = ft
+                res = self.interp_knn(points, values, grid_points=gp, shape=tshape, method=method, k=k,
+                                      power=power, eps=eps, fluid_mask=fm, flags=flags,
+                                      cell_occupancy=cell_occupancy, r0_scale=r0_scale,
+                                      lattice_bounds=lattice_bounds)
+                return tuple(unpad(a) for a in res)
+            nz, ny, nx = shape
             keep += gp
             G = Grid(nx, ny, nz, None, None, None, as_dp(gp[0]), as_dp(gp[1]), as_dp(gp[2]), 0, nz)
         z0, z1 = (0, nz) if z_range is None else z_range
@@ -401,8 +427,15 @@ class Context:
             keep += [ax, ay, az]
             G = Grid(nx, ny, nz, as_dp(ax), as_dp(ay), as_dp(az), None, None, None, 0, nz)
         else:
-            nz, ny, nx = shape
             gp = [np.ascontiguousarray(a, dtype=np.float64).ravel() for a in grid_points]
+            ft = _flat_tiles(gp, shape, fluid_mask, z_range)
+            if ft is not None:
+                gp, tshape, fm, unpad = ft
+                res = self.interp_rbf(points, values, grid_points=gp, shape=tshape, k=k, kernel=kernel,
+                                      epsilon=epsilon, degree=degree, smoothing=smoothing, fluid_mask=fm,
+                                      flags=flags, chunk_planes=chunk_planes)
+                return tuple(unpad(a) for a in res)
+            nz, ny, nx = shape
             keep += gp
             G = Grid(nx, ny, nz, None, None, None, as_dp(gp[0]), as_dp(gp[1]), as_dp(gp[2]), 0, nz)
         z0, z1 = (0, nz) if z_range is None else z_range
