@@ -207,6 +207,8 @@ int ptv_version(void);
 /* sizeof(ptv_particles, ptv_grid, ptv_knn_params, ptv_stats, ptv_rbf_params, ptv_div_params):
  * binding self-check */
 int ptv_abi_sizes(int64_t out6[6]);
+/* sizeof(ptv_mask_grid, ptv_boundary_params, ptv_filter_params): the same self-check */
+int ptv_abi_sizes2(int64_t out3[3]);
 const char *ptv_last_error(void);
 int ptv_device_count(int *out);
 int ptv_init(int device, ptv_ctx **out);

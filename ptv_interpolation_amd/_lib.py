@@ -117,6 +117,7 @@ class Stats(C.Structure):
 EXPORTS = {
     "ptv_version": (C.c_int, []),
     "ptv_abi_sizes": (C.c_int, [C.POINTER(C.c_int64)]),
+    "ptv_abi_sizes2": (C.c_int, [C.POINTER(C.c_int64)]),
     "ptv_last_error": (C.c_char_p, []),
     "ptv_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "ptv_init": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
@@ -198,6 +199,13 @@ def abi_sizes():
     py = [C.sizeof(Particles), C.sizeof(Grid), C.sizeof(KnnParams), C.sizeof(Stats), C.sizeof(RbfParams),
           C.sizeof(DivParams)]
     return list(out), py
+
+
+def abi_sizes2():
+    """(C sizeof, ctypes sizeof) of the pore-mask / filter structs."""
+    out = (C.c_int64 * 3)()
+    check(lib().ptv_abi_sizes2(out))
+    return list(out), [C.sizeof(MaskGrid), C.sizeof(BoundaryParams), C.sizeof(FilterParams)]
 
 
 def device_count() -> int:

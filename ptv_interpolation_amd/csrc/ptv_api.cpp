@@ -113,6 +113,17 @@ int ptv_abi_sizes(int64_t out6[6]) {
     return PTV_OK;
 }
 
+int ptv_abi_sizes2(int64_t out3[3]) {
+    if (!out3) {
+        set_error("ptv_abi_sizes2: out is NULL");
+        return PTV_E_ARG;
+    }
+    out3[0] = (int64_t)sizeof(ptv_mask_grid);
+    out3[1] = (int64_t)sizeof(ptv_boundary_params);
+    out3[2] = (int64_t)sizeof(ptv_filter_params);
+    return PTV_OK;
+}
+
 const char *ptv_last_error(void) { return g_last_error.c_str(); }
 
 int ptv_device_count(int *out) {

@@ -41,6 +41,8 @@ def test_version_matches_header():
 def test_struct_layouts_agree():
     c, py = _lib.abi_sizes()
     assert c == py
+    c2, py2 = _lib.abi_sizes2()
+    assert c2 == py2
 
 
 def test_no_gpu_fails_loudly():
