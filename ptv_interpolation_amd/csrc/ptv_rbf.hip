@@ -44,6 +44,16 @@
 
 namespace ptv {
 
+// 1/p from v_rcp_f64 and two Newton steps (within an ulp of the IEEE quotient; the
+// elimination multiplier l = a * (1/p) is LAPACK dgetf2's reciprocal scaling anyway)
+__device__ __forceinline__ double rcp_nr(double p) {
+    double r = __builtin_amdgcn_rcp(p);
+    double e = fma(-p, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-p, r, 1.0);
+    return fma(r, e, r);
+}
+
 __device__ __forceinline__ void rbf_wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -368,7 +378,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M <= 32 ? 3
         const double piv = prow_buf[c];
         const bool upd = !done && !isP;
         if (upd && pos == c) pos = (int)prow_buf[M + 3];  // the swap moves this row to the pivot's position
-        const double l = (upd && piv != 0.0) ? A[c] * (1.0 / piv) : 0.0;
+        const double l = (upd && piv != 0.0) ? A[c] * rcp_nr(piv) : 0.0;
 #pragma unroll
         for (int j = c + 1; j < M; ++j) A[j] = fma(-l, prow_buf[j], A[j]);
         b0 = fma(-l, prow_buf[M], b0);
