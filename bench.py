@@ -1,35 +1,46 @@
 #!/usr/bin/env python3
-"""Headline benchmark: k-NN IDW of 5M sphere-pack particles onto a 512^3 grid (fp64).
+"""Benchmark of the MI355X scattered-to-grid interpolator (BASELINE.json metric and configs).
 
-Metric (BASELINE.json): Mvoxels/s interpolated + achieved HBM GB/s, 512^3 grid /
-5M particles IDW.  One *step* = one full pass of the hot path with every input
-already resident in HBM: bounding box + particle binning + coarse-lattice bounds +
-the k-NN IDW kernel writing U, V, W (the reference rebuilds its KDTree on every
-call, interpolator.py:132, so the binning is inside the step).
+Headline (the default; BASELINE metric): k-NN IDW (k = 8, p = 2, fp64) of 5M sphere-pack
+particles onto a 512^3 grid.  One *step* = one pass of the hot path with every input already
+resident in HBM: bounding box + particle binning + coarse-lattice bounds + the k-NN IDW kernel
+writing U, V, W (the reference rebuilds its KDTree on every call, interpolator.py:132, so the
+binning is inside the step).
 
-    python bench.py [--gpus N --steps K --warmup W]
-    torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
+    python bench.py [--gpus N --steps K --warmup W] [--config headline|c2|c3|c4|c5]
+    torchrun --nproc-per-node N bench.py --gpus N ...          (one process per GPU, RCCL)
 
-Multi-GPU (weak scaling): rank r owns z-slab copy r of a stack of
-sphere packs along z (grid 512 x 512 x 512N, 5M particles per copy); it bins its
-own copy plus the particles of the neighbouring copies within `--halo` voxels of
-its slab and interpolates its 512^3 slab.  No collective touches the data path;
-the barrier + max-over-ranks timing uses torch.distributed (RCCL).
-`value` = all voxels of all ranks / max rank time.
+Multi-GPU = the north_star partition (zslab.py): ONE grid cut into z-slabs,
+rank r computing planes slab_bounds(nz, N)[r], the particle set replicated in every rank's HBM
+(all-gather / broadcast before the timed loop) and culled on device to the slab's window with
+a proof of exactness (ptv_knn_params.slab_halo; a failed proof widens the halo, never changes
+a result).  No collective touches the timed step; an RCCL all-gather reassembly of the full
+field is timed once after it and reported apart (``allgather_ms``).
 
-Rank 0 prints ONE JSON line.  `roofline.achieved` = algorithmic bytes of the k-NN
-kernel, V*(6k+3)*8 (SURVEY.md §8(d) gather model), / its hipEvent-timed average
-duration.  `roofline.traffic` is read from profiles/traffic_*.json (rocprofv3
-FETCH_SIZE/WRITE_SIZE passes, tools/collect_traffic.sh) when present.
-`cpu_baseline` times the oracle restatement of interpolator.py:126-155
-(scipy KDTree + numpy) over z-slabs on a ProcessPoolExecutor — the
-interpolator.py:173-182 / test_parallel.py multiprocess pattern — on a bounded
-sample of the same workload.
+* headline: weak scaling.  The grid is 512 x 512 x 512N: N stacked sphere-pack copies along z
+  (5M particles each, all 5M N replicated on every rank), rank r owns copy r's 512^3 planes.
+* c2 (256^3 / 1M IDW), c3 (512^3 / 5M local Gaussian RBF 32 x 32), c4 (1024^3 / 10M IDW with
+  the sphere-pack pore mask fused), c5 (2048^3 / 50M IDW, float32 field, + the consistent
+  divergence of view_divergence.py over each slab with a one-plane halo interpolated
+  redundantly): strong scaling of the named grid, the configs' N = 1 line being the whole grid
+  on one GPU.
+
+Rank 0 prints ONE JSON line.  ``roofline.achieved`` = algorithmic bytes of the k-NN kernel
+(SURVEY.md §8(d) gather model, V (6k 8 + 3 s_out) for this rank's slab) / its hipEvent-timed
+average duration; ``roofline.frac_step`` divides the step's bytes (+ 48 B per binned particle)
+by bin + cull + lattice + k-NN time.  ``cpu_baseline`` times the oracle restatement of
+interpolator.py:126-155 (scipy KDTree + numpy) over z-slabs on a ProcessPoolExecutor — the
+interpolator.py:173-182 / test_parallel.py pattern — on a bounded sample of the same workload,
+with the CPU model and the calibration against the reference (profiles/cpu_calibration_*.json).
+``--method div|filter|mask`` bench the rows next to the path (physics.py / filtering.py /
+the pore-mask path) with their own metric lines.
 """
 from __future__ import annotations
 
 import argparse
+import contextlib
 import glob
+import io
 import json
 import math
 import os
@@ -42,13 +53,33 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "Mvoxels/s interpolated + achieved HBM GB/s, 512³ grid / 5M particles IDW"
+METRIC_C2 = "Mvoxels/s interpolated + achieved HBM GB/s, 256³ grid / 1M particles IDW"
+METRIC_RBF = "Mvoxels/s interpolated + achieved FP64 TFLOP/s, 512³ grid / 5M particles local RBF"
+METRIC_C4 = "Mvoxels/s interpolated + achieved HBM GB/s, 1024³ grid / 10M particles masked IDW (z-slab partition)"
+METRIC_C5 = ("Mvoxels/s interpolated + achieved HBM GB/s, 2048³ grid / 50M particles fp32 IDW + divergence "
+             "(z-slab partition)")
 METRIC_DIV = "Mvoxels/s + achieved HBM GB/s, consistent divergence (physics.py:6-53) of a 512³ field"
 METRIC_FILTER = "Mparticles/s filtered + achieved HBM GB/s, k-NN median/MAD outlier filter (filtering.py:5-58), 5M particles"
 METRIC_MASK = ("Mvoxels/s + achieved HBM GB/s, pore-mask path (sample_mask_on_grid + extract_boundary_particles, "
                "interpolator.py:205-284), 512³ mask")
-METRIC_RBF = "Mvoxels/s interpolated + achieved FP64 TFLOP/s, 512³ grid / 5M particles local RBF"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec (AMD); not listed in the guide
+KMAX_LIST = (4, 8, 12, 16, 24, 32, 40, 48, 56, 64)  # k_knn_interp instantiations (ptv_knn.hip)
+
+# BASELINE.json configs; C1 (64^3 / 10k, CPU plumbing) is a parity test case
+CONFIGS = {
+    "headline": dict(grid=512, particles=5_000_000, method="idw", k=8, scaling="weak", metric=METRIC),
+    "c2": dict(grid=256, particles=1_000_000, method="idw", k=8, scaling="strong", metric=METRIC_C2),
+    "c3": dict(grid=512, particles=5_000_000, method="rbf", k=32, rbf_kernel="gaussian", epsilon=0.3, degree=-1,
+               scaling="strong", metric=METRIC_RBF),
+    "c4": dict(grid=1024, particles=10_000_000, method="idw", k=8, mask=True, scaling="strong", metric=METRIC_C4),
+    "c5": dict(grid=2048, particles=50_000_000, method="idw", k=8, out_dtype="f32", div=True, scaling="strong",
+               metric=METRIC_C5),
+}
+
+
+def kmax_for(k):
+    return next((m for m in KMAX_LIST if k <= m), 0)
 
 
 def rbf_resolved(args):
@@ -72,50 +103,78 @@ def rbf_flops_per_voxel(k, m):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--grid", type=int, default=512)
-    ap.add_argument("--particles", type=int, default=5_000_000)
-    ap.add_argument("--k", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default 20; 5 for c3, c5)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 5; 2 for c3, c5)")
+    ap.add_argument("--config", default="headline", choices=sorted(CONFIGS))
+    ap.add_argument("--grid", type=int, default=None)
+    ap.add_argument("--particles", type=int, default=None)
+    ap.add_argument("--k", type=int, default=None)
     ap.add_argument("--power", type=float, default=2.0)
-    ap.add_argument("--method", default="idw", choices=["idw", "sibson", "nearest", "rbf", "div", "filter", "mask"])
+    ap.add_argument("--method", default=None, choices=["idw", "sibson", "nearest", "rbf", "div", "filter", "mask"])
     ap.add_argument("--div-dtype", default="f64", choices=["f64", "f32"],
                     help="--method div: field dtype (f32 = the C5 fp32 field, Python-float spacings)")
-    ap.add_argument("--rbf-kernel", default="thin_plate_spline", help="--method rbf: scipy kernel name")
-    ap.add_argument("--epsilon", type=float, default=None, help="--method rbf: shape parameter")
-    ap.add_argument("--degree", type=int, default=None, help="--method rbf: polynomial degree")
-    ap.add_argument("--out-dtype", default="f64", choices=["f64", "f32"],
+    ap.add_argument("--rbf-kernel", default=None, help="rbf: scipy kernel name (default thin_plate_spline)")
+    ap.add_argument("--epsilon", type=float, default=None, help="rbf: shape parameter")
+    ap.add_argument("--degree", type=int, default=None, help="rbf: polynomial degree")
+    ap.add_argument("--out-dtype", default=None, choices=["f64", "f32"],
                     help="k-NN methods: U, V, W stored as float32 (PTV_FLAG_OUT_F32, the fused main.py:230 "
-                         "astype; arithmetic stays f64) — the C5 configuration's field")
-    ap.add_argument("--mask", action="store_true",
-                    help="k-NN methods: sphere-pack fluid mask + NaN fill fused (main.py:195-207; the C4 masked "
-                         "geometry): solid voxels are skipped and written as 0")
+                         "astype; arithmetic stays f64)")
+    ap.add_argument("--mask", action="store_true", default=None,
+                    help="k-NN methods: sphere-pack fluid mask + NaN fill fused (main.py:195-207): solid voxels "
+                         "are skipped and written as 0")
+    ap.add_argument("--div", action="store_true", default=None,
+                    help="k-NN methods: + consistent divergence of each slab (C5)")
+    ap.add_argument("--halo", type=float, default=None, help="N>1: first slab_halo to try (default: 4 k-NN radii)")
     ap.add_argument("--r0-scale", type=float, default=0.0, help="dev: first search radius / expected k-NN radius")
-    ap.add_argument("--halo", type=int, default=64, help="neighbour-copy halo (voxels) for N>1")
-    ap.add_argument("--cpu-sample-planes", type=int, default=16)
-    ap.add_argument("--cpu-workers", type=int, default=16)
+    ap.add_argument("--cpu-sample-planes", type=int, default=None)
+    ap.add_argument("--cpu-workers", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--allgather", action="store_true", help="also time an RCCL all-gather of U,V,W (reported apart)")
-    return ap.parse_args()
+    ap.add_argument("--no-allgather", action="store_true", help="N>1: skip the timed RCCL all-gather reassembly")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer end-to-end interpolate_field timing")
+    a = ap.parse_args()
+    cfg = CONFIGS[a.config]
+    defaults = dict(grid=cfg["grid"], particles=cfg["particles"], method=cfg["method"], k=cfg["k"],
+                    rbf_kernel=cfg.get("rbf_kernel", "thin_plate_spline"), epsilon=cfg.get("epsilon"),
+                    degree=cfg.get("degree"), out_dtype=cfg.get("out_dtype", "f64"), mask=cfg.get("mask", False),
+                    div=cfg.get("div", False))
+    for key, v in defaults.items():
+        if getattr(a, key) is None:
+            setattr(a, key, v)
+    heavy = a.config in ("c3", "c5")
+    a.steps = a.steps if a.steps is not None else (5 if heavy else 20)
+    a.warmup = a.warmup if a.warmup is not None else (2 if heavy else 5)
+    a.scaling = cfg["scaling"]
+    a.metric = cfg["metric"]
+    return a
 
 
-def rank_particles(args, rank, world, values="reference"):
-    """Particles of pack copy `rank` plus halo particles of copies rank+-1 (weak scaling)."""
-    from ptv_interpolation_amd import synth
+# ---------------------------------------------------------------------------------------------
+# CPU baseline context: the host's CPU model, and the calibration of the oracle against the
+# reference in the build container (tools/cpu_calibration.py)
+# ---------------------------------------------------------------------------------------------
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
 
-    G = args.grid
-    P, Q = synth.sphere_pack(args.particles, G, values=values, z_tiles=world, z_tile=rank)
-    if world == 1:
-        return P, Q
-    parts, vals = [P], [Q]
-    z_lo, z_hi = rank * G, (rank + 1) * G
-    for nb in (rank - 1, rank + 1):
-        if 0 <= nb < world:
-            Pn, Qn = synth.sphere_pack(args.particles, G, values=values, z_tiles=world, z_tile=nb)
-            keep = (Pn[:, 2] >= z_lo - args.halo) & (Pn[:, 2] < z_hi + args.halo)
-            parts.append(Pn[keep])
-            vals.append(Qn[keep])
-    return np.concatenate(parts), np.concatenate(vals)
+    return platform.processor() or "unknown"
+
+
+def cpu_calibration():
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "cpu_calibration_*.json")))
+    if not files:
+        return None
+    try:
+        with open(files[-1]) as f:
+            c = json.load(f)
+        return {"file": os.path.relpath(files[-1], ROOT), "ratios": c.get("ratios"), "within_15pct": c.get("within_15pct")}
+    except Exception:
+        return None
 
 
 def row_traffic(*keys):
@@ -132,8 +191,8 @@ def row_traffic(*keys):
         return None
 
 
-def traffic_from_profiles(kernel_substr="k_knn_interp<"):
-    """HBM bytes per k-NN launch from the newest profiles/traffic_*.json (or None)."""
+def traffic_from_profiles():
+    """HBM bytes per main k-NN launch at the headline from the newest profiles/traffic_rNN.json."""
     import re
 
     files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "traffic_r*.json"))
@@ -148,23 +207,28 @@ def traffic_from_profiles(kernel_substr="k_knn_interp<"):
         return None
 
 
-def cpu_baseline(args, P, Q, ax):
+def _cpu_line(value, unit, workers, sample, dt):
+    return {"value": value, "unit": unit, "cores": workers, "kind": "port", "sample": sample, "seconds": round(dt, 2),
+            "cpu_model": cpu_model(), "calibration": cpu_calibration()}
+
+
+def cpu_baseline(args, P, Q, ax, az, z0_grid):
     """Oracle restatement on a bounded z-slab sample, multiprocess (test_parallel.py pattern)."""
     from oracle import cpu_ref
 
-    planes = min(args.cpu_sample_planes, len(ax))
-    z0 = len(ax) // 2 - planes // 2
-    workers = max(1, min(args.cpu_workers, os.cpu_count() or 1))
+    big = args.particles > 20_000_000
+    planes = min(args.cpu_sample_planes or (4 if big else 16), len(az))
+    workers = max(1, min(args.cpu_workers or (4 if big else 16), os.cpu_count() or 1))
+    z0 = z0_grid + len(az) // 2 - planes // 2
     t = time.perf_counter()
-    cpu_ref.interp_grid_parallel(P, Q, ax, ax, ax, args.method, args.k, args.power,
+    cpu_ref.interp_grid_parallel(P, Q, ax, ax, az, args.method, args.k, args.power,
                                  z0=z0, z1=z0 + planes, n_jobs=workers, slab=max(1, planes // workers))
     dt = time.perf_counter() - t
     nvox = planes * len(ax) * len(ax)
-    return {"value": round(nvox / dt / 1e6, 4), "unit": "Mvoxels/s", "cores": workers, "kind": "port",
-            "sample": f"{planes} central z-planes ({nvox} voxels) of the same {args.grid}^3/"
-                      f"{args.particles} workload; scipy KDTree + numpy (oracle/cpu_ref.py), "
-                      f"{workers} processes, each building its own tree (interpolator.py:173-182 pattern)",
-            "seconds": round(dt, 2)}
+    return _cpu_line(round(nvox / dt / 1e6, 4), "Mvoxels/s", workers,
+                     f"{planes} central z-planes ({nvox} voxels) of the same {args.grid}^3/{args.particles} workload "
+                     f"(mask not applied); scipy KDTree + numpy (oracle/cpu_ref.py), {workers} processes, each "
+                     f"building its own tree (interpolator.py:173-182 pattern)", dt)
 
 
 def _rbf_cpu_worker(a):
@@ -180,7 +244,7 @@ def cpu_baseline_rbf(args, P, Q, ax):
     from concurrent.futures import ProcessPoolExecutor
 
     kern, eps, deg, _ = rbf_resolved(args)
-    workers = max(1, min(args.cpu_workers, os.cpu_count() or 1))
+    workers = max(1, min(args.cpu_workers or 16, os.cpu_count() or 1))
     nvox = 2048 * workers
     G = len(ax)
     rng = np.random.default_rng(0)
@@ -191,11 +255,300 @@ def cpu_baseline_rbf(args, P, Q, ax):
     with ProcessPoolExecutor(max_workers=workers) as ex:
         list(ex.map(_rbf_cpu_worker, [(P, Q, c, args.k, kern, eps, deg) for c in np.array_split(q, workers)]))
     dt = time.perf_counter() - t
-    return {"value": round(nvox / dt / 1e6, 6), "unit": "Mvoxels/s", "cores": workers, "kind": "port",
-            "sample": f"{nvox} random voxels of the same {G}^3/{args.particles} workload; scipy KDTree + numpy "
-                      f"LAPACK gesv per voxel (oracle/cpu_ref.rbf_local_points), {workers} processes, each "
-                      f"building its own tree (interpolator.py:173-182 pattern)",
-            "seconds": round(dt, 2)}
+    return _cpu_line(round(nvox / dt / 1e6, 6), "Mvoxels/s", workers,
+                     f"{nvox} random voxels of the same {G}^3/{args.particles} workload; scipy KDTree + numpy "
+                     f"LAPACK gesv per voxel (oracle/cpu_ref.rbf_local_points), {workers} processes, each "
+                     f"building its own tree (interpolator.py:173-182 pattern)", dt)
+
+
+def _dist_init():
+    """One process per GPU (torchrun env); returns (world, rank, local, dist or None, device)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local, dist, torch.device("cuda", local)
+
+
+def _timed(step, args, dist, dev, stat_key, ctx):
+    """W warmup steps, then K steps between barriers + synchronize; (max-over-ranks seconds, kernel ms list)."""
+    import torch
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    k_ms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        k_ms.append(ctx.last_stats()[stat_key] if stat_key else 0.0)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, k_ms
+
+
+# ---------------------------------------------------------------------------------------------
+# the interpolation benches (headline, c2-c5)
+# ---------------------------------------------------------------------------------------------
+def _device_fluid_mask(G, nz_grid, planes, dev):
+    """uint8 (nz_grid, G, G) device tensor: the sphere-pack fluid mask (synth.fluid_mask; stacked
+    copies repeat it along z) on planes [a, b), zero elsewhere (never read)."""
+    import torch
+
+    from ptv_interpolation_amd import synth
+
+    m = torch.zeros((nz_grid, G, G), dtype=torch.uint8, device=dev)
+    a, b = planes
+    for z in range(a, b, 64):
+        zz = min(b, z + 64)
+        m[z:zz] = synth.fluid_mask_device(G, z, zz, dev)
+    return m
+
+
+def main_interp(args):
+    import torch
+
+    world, rank, local, dist, dev = _dist_init()
+    from ptv_interpolation_amd import _lib, synth, zslab
+
+    G, k = args.grid, args.k
+    rbf = args.method == "rbf"
+    weak = args.scaling == "weak"
+    if args.method == "nearest":
+        k = args.k = 1
+    nz = G * world if weak else G
+    z0, z1 = (rank * G, (rank + 1) * G) if weak else zslab.rank_slab(G, world, rank)
+    za, zb, hlo, hhi = zslab.halo_slab(z0, z1, nz, 1 if args.div else 0)
+
+    # particles: replicated on every rank (north_star); weak: copy r generated by rank r and
+    # all-gathered; strong: generated by rank 0 and broadcast
+    def cols_of(P, Q):
+        return [torch.from_numpy(np.ascontiguousarray(P[:, i])).to(dev) for i in range(3)] + \
+               [torch.from_numpy(np.ascontiguousarray(Q[:, i])).to(dev) for i in range(3)]
+
+    P = Q = None
+    if weak:
+        P, Q = synth.sphere_pack(args.particles, G, z_tiles=world, z_tile=rank)
+        cols = zslab.replicate_columns(cols_of(P, Q), dist)
+    elif rank == 0:
+        P, Q = synth.sphere_pack(args.particles, G)
+        cols = zslab.broadcast_columns(cols_of(P, Q), dist)
+    else:
+        cols = zslab.broadcast_columns([torch.empty(args.particles, dtype=torch.float64, device=dev)
+                                        for _ in range(6)], dist)
+    n = cols[0].numel()
+    ax_h = np.linspace(0, G - 1, G)
+    az_h = np.linspace(0, nz - 1, nz)
+    axes = [torch.from_numpy(ax_h).to(dev), torch.from_numpy(ax_h.copy()).to(dev), torch.from_numpy(az_h).to(dev)]
+    out_f32 = args.out_dtype == "f32" and not rbf
+    odt = torch.float32 if out_f32 else torch.float64
+    out = [torch.empty((zb - za, G, G), dtype=odt, device=dev) for _ in range(3)]
+    mask_t = None
+    fluid_frac = None
+    if args.mask or args.div:
+        mask_t = _device_fluid_mask(G, nz, (za, zb), dev)
+        fluid_frac = float(mask_t[z0:z1].float().mean().item())
+    div_out = torch.empty((z1 - z0, G, G), dtype=odt, device=dev) if args.div else None
+    ctx = _lib.Context(local)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    method = {"idw": _lib.METHOD_IDW, "sibson": _lib.METHOD_SIBSON, "nearest": _lib.METHOD_NEAREST}.get(args.method)
+    cull = world > 1 and not rbf
+    halo = zslab.HaloState(args.halo if args.halo is not None else
+                           zslab.halo_guess(n, (G, G, nz), k))
+    ptrs = [c.data_ptr() for c in cols]
+    aptrs = [a.data_ptr() for a in axes]
+    optrs = [o.data_ptr() for o in out]
+    if rbf:
+        kern, eps, deg, m_sys = rbf_resolved(args)
+
+    def step():
+        if rbf:
+            ctx.interp_rbf_dev(n, ptrs, G, G, nz, axes_ptrs=aptrs, out_ptrs=optrs, k=k, kernel=kern, epsilon=eps,
+                               degree=deg, z_range=(za, zb), stream=stream)
+            return
+        flags = (_lib.FLAG_OUT_F32 if out_f32 else 0) | (_lib.FLAG_NAN_TO_NUM if args.mask else 0)
+        mptr = mask_t.data_ptr() if (mask_t is not None and args.mask) else 0
+
+        def call(h):
+            return ctx.interp_knn_dev(n, ptrs, G, G, nz, axes_ptrs=aptrs, out_ptrs=optrs, method=method, k=k,
+                                      power=args.power, stream=stream, mask_ptr=mptr, r0_scale=args.r0_scale,
+                                      flags=flags, z_range=(za, zb), slab_halo=h)
+
+        zslab.interp_slab(call, halo) if cull else call(0.0)
+        if args.div:
+            dtc = _lib.F32 if out_f32 else _lib.F64
+            ctx.divergence_dev(G, G, zb - za, [o.data_ptr() for o in out], mask_t[za:zb].data_ptr(),
+                               div_out.data_ptr(), 1.0, 1.0, 1.0, field_dtype=dtc, result_dtype=dtc,
+                               z_range=(hlo, hlo + (z1 - z0)), edges=(hlo == 0, hhi == 0), stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    rec = {key: [] for key in ("ms_knn", "ms_lattice", "ms_bin", "ms_solve", "ms_cull", "ms_stencil", "n_binned")}
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        st = ctx.last_stats()  # synchronises on the step's events
+        for key in rec:
+            rec[key].append(st[key])
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    avg = {key: float(np.mean(v)) for key, v in rec.items()}
+
+    # RCCL all-gather reassembly of the full field, once, reported apart from `value`
+    gather_ms = None
+    if dist is not None and not args.no_allgather and all((b - a) == (z1 - z0) for a, b in
+                                                          [zslab.rank_slab(nz, world, r) for r in range(world)]):
+        try:
+            torch.cuda.synchronize(dev)
+            dist.barrier()
+            tg = time.perf_counter()
+            for o in out:
+                full = zslab.gather_field(o[hlo:hlo + (z1 - z0)], dist)
+                del full
+            torch.cuda.synchronize(dev)
+            gather_ms = (time.perf_counter() - tg) * 1e3
+        except Exception as e:  # the reassembly must never take the bench line down
+            gather_ms = repr(e)[:200]
+
+    # end-to-end through the drop-in (host DataFrame in, host float64 U, V, W out): H2D +
+    # binning + kernels + D2H, what a main.py user pays (N = 1, unmasked k-NN configs)
+    e2e = None
+    if world == 1 and not rbf and not args.mask and not args.div and not args.no_e2e and P is not None:
+        try:
+            import pandas as pd
+
+            from ptv_interpolation_amd import interpolator as ip
+
+            df = pd.DataFrame({"x": P[:, 0], "y": P[:, 1], "z": P[:, 2], "u": Q[:, 0], "v": Q[:, 1], "w": Q[:, 2]})
+            grid, _ = ip.create_grid(((0, G), (0, G), (0, G)), G, dense=False)
+            kw = {"idw": dict(idw_neighbors=k, idw_power=args.power), "sibson": dict(sibson_neighbors=k),
+                  "nearest": {}}[args.method]
+            walls = []
+            os.environ["PTV_DEVICE"] = str(local)  # this rank's GPU only (launcher.devices())
+            for _ in range(2):  # first call allocates the context's host-path buffers
+                t = time.perf_counter()
+                with contextlib.redirect_stdout(io.StringIO()):
+                    ip.interpolate_field(df, grid, method=args.method, **kw)
+                walls.append(time.perf_counter() - t)
+            hs = _lib.Context.get(local).stats
+            e2e = {"wall_s": round(walls[-1], 3), "mvoxels_per_s": round(G ** 3 / walls[-1] / 1e6, 1),
+                   "ms_h2d": round(hs["ms_h2d"], 2), "ms_device": round(hs["ms_total"] - hs["ms_h2d"] - hs["ms_d2h"], 2),
+                   "ms_d2h": round(hs["ms_d2h"], 2),
+                   "what": "interpolate_field(DataFrame, create_grid(dense=False)) -> host float64 U, V, W; "
+                           "pageable host buffers, second call"}
+        except Exception as e:
+            e2e = {"error": repr(e)[:200]}
+
+    V_slab = (z1 - z0) * G * G
+    s_out = 4 if out_f32 else 8
+    if rbf:
+        flops = (zb - za) * G * G * rbf_flops_per_voxel(k, m_sys)
+        tf = flops / (avg["ms_solve"] * 1e-3) / 1e12
+        roof = {"bound": "fp64", "achieved": round(tf, 2), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(tf / FP64_PEAK_TFLOPS, 4), "traffic": None, "kernel": f"k_rbf_local<{(m_sys + 7) & ~7}>",
+                "alg_flops_per_launch": flops, "kernel_ms": round(avg["ms_solve"], 3),
+                "knn_slots_ms": round(avg["ms_knn"], 3)}
+    else:
+        Vk = (zb - za) * G * G  # voxels the k-NN launch computes (slab + redundant halo planes)
+        if args.mask:  # solid voxels are skipped: fluid V in the gather term, + the mask byte
+            alg = int(round(Vk * fluid_frac)) * 6 * k * 8 + Vk * (3 * s_out + 1)
+        else:
+            alg = Vk * (6 * k * 8 + 3 * s_out)
+        ach = alg / (avg["ms_knn"] * 1e-3) / 1e9
+        t_step = avg["ms_bin"] + avg["ms_cull"] + avg["ms_lattice"] + avg["ms_knn"]
+        alg_step = alg + 48 * avg["n_binned"]
+        headline_shape = (G == 512 and args.particles == 5_000_000 and k == 8 and not args.mask and not out_f32)
+        roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBPS, 4),
+                "traffic": traffic_from_profiles() if headline_shape else None,
+                "kernel": f"k_knn_interp<{kmax_for(k)}>", "alg_bytes_per_launch": alg,
+                "kernel_ms": round(avg["ms_knn"], 3),
+                "frac_step": round(alg_step / (t_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                "step_device_ms": round(t_step, 3)}
+        if args.div:
+            dalg = V_slab * (4 * s_out + 1)
+            dach = dalg / (avg["ms_stencil"] * 1e-3) / 1e9
+            roof["divergence"] = {"kernel": f"k_divergence<{'float' if out_f32 else 'double'}>",
+                                  "achieved": round(dach, 1), "frac": round(dach / HBM_PEAK_GBPS, 4),
+                                  "alg_bytes": dalg, "kernel_ms": round(avg["ms_stencil"], 4)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and P is not None:
+        try:
+            cpu = cpu_baseline_rbf(args, P, Q, ax_h) if rbf else cpu_baseline(args, P, Q, ax_h, az_h, 0)
+        except Exception as e:  # the baseline must never take the GPU line down
+            cpu = {"value": None, "error": repr(e)[:200]}
+
+    if rank == 0:
+        vox_total = V_slab * world if weak else G ** 3
+        value = vox_total / (elapsed / args.steps) / 1e6
+        if weak:
+            wl = (f"{G}x{G}x{nz} grid = {world} stacked {G}^3 sphere-pack copies / {args.particles * world} "
+                  f"particles (replicated), {G}^3 slab + {args.particles} particles' copy per GPU")
+        else:
+            wl = f"{G}^3 grid / {args.particles} particles (replicated), z-slab of {G // world if world else G} planes per GPU"
+        if rbf:
+            wl += f"; local RBF {kern} k={k} eps={eps} degree={deg} (system {m_sys}) fp64"
+        else:
+            wl += (f"; {args.method.upper()} k={k} p={args.power} fp64" + (" (float32 U, V, W)" if out_f32 else "") +
+                   (f" + sphere-pack fluid mask ({fluid_frac:.1%} fluid, solid skipped)" if args.mask else "") +
+                   (" + consistent divergence (one-plane halo interpolated)" if args.div else ""))
+        line = {
+            "metric": args.metric, "value": round(value, 2), "unit": "Mvoxels/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic: generate_sphere_pack.py geometry scaled to voxel units, seeded, w=1 flow field",
+            "config": {"workload": wl, "name": args.config, "grid": G, "grid_z": nz, "particles": args.particles,
+                       "particles_replicated": n, "method": args.method, "k": k, "power": args.power,
+                       "out_dtype": "f32" if out_f32 else "f64", "mask": bool(args.mask), "div": bool(args.div),
+                       "parallelism": f"z-slab x{world}" + (" (particles replicated, slab_halo cull)" if cull else "")},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "breakdown_ms": {"bin": round(avg["ms_bin"], 3), "cull": round(avg["ms_cull"], 3),
+                             "lattice": round(avg["ms_lattice"], 3), "knn": round(avg["ms_knn"], 3),
+                             "solve": round(avg["ms_solve"], 3), "divergence": round(avg["ms_stencil"], 3)},
+        }
+        if args.mask:
+            line["fluid_mvoxels_per_s"] = round(value * fluid_frac, 2)
+        if cull:
+            line["halo"] = {**halo.as_dict(), "particles_binned_rank0": int(avg["n_binned"])}
+        if gather_ms is not None:
+            line["allgather_ms"] = round(gather_ms, 2) if isinstance(gather_ms, float) else gather_ms
+        if e2e is not None:
+            line["e2e"] = e2e
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
 
 
 def cpu_baseline_div(args, fields, fluid):
@@ -212,6 +565,7 @@ def cpu_baseline_div(args, fields, fluid):
     dt = time.perf_counter() - t
     nvox = planes * G * G
     return {"value": round(nvox / dt / 1e6, 3), "unit": "Mvoxels/s", "cores": 1, "kind": "port",
+            "cpu_model": cpu_model(),
             "sample": f"{planes} central z-planes ({nvox} voxels) of the same {G}^3 field; numpy restatement "
                       f"of physics.compute_consistent_divergence (oracle/cpu_ref.py), 1 process",
             "seconds": round(dt, 2)}
@@ -312,50 +666,6 @@ def main_div(args):
         dist.destroy_process_group()
 
 
-def _dist_init():
-    """One process per GPU (torchrun env); returns (world, rank, local, dist or None, device)."""
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    import torch
-
-    torch.cuda.set_device(local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    return world, rank, local, dist, torch.device("cuda", local)
-
-
-def _timed(step, args, dist, dev, stat_key, ctx):
-    """W warmup steps, then K steps between barriers + synchronize; (max-over-ranks seconds, kernel ms list)."""
-    import torch
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    k_ms = []
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-        k_ms.append(ctx.last_stats()[stat_key] if stat_key else 0.0)
-    torch.cuda.synchronize(dev)
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    return elapsed, k_ms
-
-
 def main_filter(args):
     """--method filter: one step = remove_outliers_knn (filtering.py:5-58) over a resident particle set:
     binning + (k+1)-NN of every particle among the particles (slot mode) + median/MAD per particle.
@@ -397,7 +707,7 @@ def main_filter(args):
             t = time.perf_counter()
             cpu_ref.outlier_filter(P[:m], Q[:m], k, 3.0, workers=1)
             dt = time.perf_counter() - t
-            cpu = {"value": round(m / dt / 1e6, 4), "unit": "Mparticles/s", "cores": 1, "kind": "port",
+            cpu = {"value": round(m / dt / 1e6, 4), "unit": "Mparticles/s", "cores": 1, "kind": "port", "cpu_model": cpu_model(),
                    "sample": f"first {m} particles of the same cloud (a {m / n:.0%} subset at the same density "
                              "is not the same neighbourhoods; documented), scipy KDTree(k+1) + numpy median/MAD "
                              "(oracle/cpu_ref.outlier_filter = filtering.py:15-51), workers=1",
@@ -488,6 +798,7 @@ def main_mask(args):
             cpu_ref.boundary_particles(f, ((0, Gs),) * 3, 1, 1)
             dt = time.perf_counter() - t
             cpu = {"value": round(Gs ** 3 / dt / 1e6, 3), "unit": "Mvoxels/s", "cores": 1, "kind": "port",
+                   "cpu_model": cpu_model(),
                    "sample": f"{Gs}^3 sphere-pack mask, numpy restatement (oracle/cpu_ref.sample_mask_nearest + "
                              "boundary_particles of interpolator.py:205-284), 1 process",
                    "seconds": round(dt, 2)}
@@ -526,171 +837,7 @@ def main():
         return main_filter(args)
     if args.method == "mask":
         return main_mask(args)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-
-    import torch
-
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-
-    from ptv_interpolation_amd import _lib
-
-    G = args.grid
-    P, Q = rank_particles(args, rank, world)
-    n = P.shape[0]
-    ax_h = np.linspace(0, G - 1, G)
-    az_h = ax_h + rank * G
-    cols = [torch.from_numpy(np.ascontiguousarray(P[:, i])).to(dev) for i in range(3)] + \
-           [torch.from_numpy(np.ascontiguousarray(Q[:, i])).to(dev) for i in range(3)]
-    axes = [torch.from_numpy(ax_h).to(dev), torch.from_numpy(ax_h.copy()).to(dev), torch.from_numpy(az_h).to(dev)]
-    out_f32 = args.out_dtype == "f32" and args.method != "rbf"
-    mask_t = None
-    if args.mask:
-        from ptv_interpolation_amd import synth as _synth
-
-        fm = _synth.fluid_mask(G)
-        fluid_frac = float(fm.mean())
-        mask_t = torch.from_numpy(np.ascontiguousarray(fm).view(np.uint8)).to(dev)
-        del fm
-    out = [torch.empty((G, G, G), dtype=torch.float32 if out_f32 else torch.float64, device=dev) for _ in range(3)]
-    ctx = _lib.Context(local)
-    method = {"idw": _lib.METHOD_IDW, "sibson": _lib.METHOD_SIBSON, "nearest": _lib.METHOD_NEAREST}.get(args.method)
-    if args.method == "nearest":
-        args.k = 1
-    stream = torch.cuda.current_stream(dev).cuda_stream
-
-    if args.method == "rbf":
-        kern, eps, deg, m_sys = rbf_resolved(args)
-
-        def step():
-            return ctx.interp_rbf_dev(n, [c.data_ptr() for c in cols], G, G, G,
-                                      axes_ptrs=[a.data_ptr() for a in axes],
-                                      out_ptrs=[o.data_ptr() for o in out], k=args.k, kernel=kern, epsilon=eps,
-                                      degree=deg, stream=stream)
-    else:
-        def step():
-            return ctx.interp_knn_dev(n, [c.data_ptr() for c in cols], G, G, G,
-                                      axes_ptrs=[a.data_ptr() for a in axes],
-                                      out_ptrs=[o.data_ptr() for o in out], method=method, k=args.k,
-                                      power=args.power, stream=stream,
-                                      mask_ptr=mask_t.data_ptr() if mask_t is not None else 0,
-                                      r0_scale=args.r0_scale,
-                                      flags=(_lib.FLAG_OUT_F32 if out_f32 else 0) |
-                                            (_lib.FLAG_NAN_TO_NUM if mask_t is not None else 0))
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    knn_ms, lat_ms, bin_ms, solve_ms = [], [], [], []
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-        st = ctx.last_stats()  # synchronises on the step's events
-        knn_ms.append(st["ms_knn"])
-        lat_ms.append(st["ms_lattice"])
-        bin_ms.append(st["ms_bin"])
-        solve_ms.append(st["ms_solve"])
-    torch.cuda.synchronize(dev)
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    gather_ms = None
-    if args.allgather and dist is not None:
-        full = [torch.empty((G * world, G, G), dtype=out[0].dtype, device=dev) for _ in range(3)]
-        torch.cuda.synchronize(dev)
-        dist.barrier()
-        tg = time.perf_counter()
-        for c in range(3):
-            dist.all_gather_into_tensor(full[c], out[c])
-        torch.cuda.synchronize(dev)
-        gather_ms = (time.perf_counter() - tg) * 1e3
-        del full
-
-    vox = G ** 3
-    ms_step = elapsed / args.steps * 1e3
-    value = vox * world / (elapsed / args.steps) / 1e6
-    knn_avg = float(np.mean(knn_ms))
-    alg_bytes = vox * ((6 * args.k) * 8 + 3 * (4 if out_f32 else 8))
-    if args.mask:  # solid voxels are skipped, fluid V in the gather term; + the mask bytes
-        alg_bytes = int(round(vox * fluid_frac)) * (6 * args.k) * 8 + vox * (3 * (4 if out_f32 else 8) + 1)
-    achieved = alg_bytes / (knn_avg * 1e-3) / 1e9
-    traffic = traffic_from_profiles()
-
-    if args.method == "rbf":
-        solve_avg = float(np.mean(solve_ms))
-        flops = vox * rbf_flops_per_voxel(args.k, m_sys)
-        tf = flops / (solve_avg * 1e-3) / 1e12
-        roof = {"bound": "fp64", "achieved": round(tf, 2), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(tf / FP64_PEAK_TFLOPS, 4), "traffic": None, "kernel": "k_rbf_local",
-                "alg_flops_per_launch": flops, "kernel_ms": round(solve_avg, 3)}
-    else:
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": traffic, "kernel": f"k_knn_interp<{args.k}>",
-                "alg_bytes_per_launch": alg_bytes, "kernel_ms": round(knn_avg, 3)}
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        try:
-            cpu = (cpu_baseline_rbf if args.method == "rbf" else cpu_baseline)(args, P, Q, ax_h)
-        except Exception as e:  # the baseline must never take the GPU line down
-            cpu = {"value": None, "error": repr(e)[:200]}
-
-    if rank == 0:
-        line = {
-            "metric": METRIC_RBF if args.method == "rbf" else METRIC,
-            "value": round(value, 2),
-            "unit": "Mvoxels/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_step, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic: generate_sphere_pack.py geometry scaled to voxel units, seeded, w=1 flow field",
-            "config": {"workload": (f"{G}^3 grid / {args.particles} particles local RBF {kern} k={args.k} "
-                                    f"eps={eps} degree={deg} (system {m_sys}) fp64 (z-slab per GPU)")
-                       if args.method == "rbf" else
-                       f"{G}^3 grid / {args.particles} particles {args.method.upper()} "
-                       f"k={args.k} p={args.power} fp64" + (" (float32 U, V, W)" if out_f32 else "") +
-                       (f" + sphere-pack fluid mask ({fluid_frac:.1%} fluid, solid skipped)" if args.mask else "") +
-                       " (z-slab per GPU)",
-                       "grid": G, "particles": args.particles, "particles_binned_rank0": n,
-                       "method": args.method, "k": args.k, "power": args.power,
-                       "parallelism": f"z-slab x{world}"},
-            "roofline": roof,
-            "cpu_baseline": cpu,
-            **({"fluid_mvoxels_per_s": round(value * fluid_frac, 2)} if args.mask else {}),
-            "breakdown_ms": {"bin": round(float(np.mean(bin_ms)), 3), "lattice": round(float(np.mean(lat_ms)), 3),
-                             "knn": round(knn_avg, 3), "solve": round(float(np.mean(solve_ms)), 3)},
-        }
-        if gather_ms is not None:
-            line["allgather_ms"] = round(gather_ms, 2)
-        print(json.dumps(line), flush=True)
-    ctx.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    return main_interp(args)
 
 
 if __name__ == "__main__":

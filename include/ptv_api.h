@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define PTV_API_VERSION 4
+#define PTV_API_VERSION 5
 
 /* error codes */
 #define PTV_OK 0
@@ -32,7 +32,7 @@ extern "C" {
 #define PTV_E_HIP -2      /* HIP runtime / launch failure (RuntimeError)    */
 #define PTV_E_NOMEM -3    /* device allocation failed (MemoryError)         */
 #define PTV_E_UNSUPPORTED -4 /* valid but not implemented on the GPU path  */
-#define PTV_E_INEXACT -5  /* a slab-culled particle set could not prove exactness */
+#define PTV_E_INEXACT -5  /* slab_halo too small to prove the culled set exact (see ptv_knn_params) */
 #define PTV_E_SINGULAR -6 /* local RBF system singular (Python: LinAlgError) */
 
 /* interpolation methods (interpolator.py:83, :126, :157, :197) */
@@ -103,6 +103,16 @@ typedef struct {
     double cell_occupancy; /* target particles per binning cell, <=0: default */
     double r0_scale;       /* first search radius / expected k-NN radius, <=0: default */
     int lattice_bounds;    /* >=0: coarse-lattice k-th distance bounds (default), <0: off */
+    /* Multi-GPU z-slab with the particle set replicated: > 0 bins only the
+     * particles whose z lies within slab_halo of the slab's z extent [az[z_begin], az[z_end-1]]
+     * (separable grids; order-preserving on-device compaction).  Exactness is then PROVEN
+     * before the main kernel: from the finest lattice's k-th distance bounds D(c) every slab
+     * voxel v has d_k(v) <= D(c) + |v - c|, and a particle outside the window is farther than
+     * slab_halo + (v's distance to the nearer slab face); the call computes the halo that
+     * guarantees this (ptv_stats.halo_required) and returns PTV_E_INEXACT without running the
+     * interpolation when slab_halo is smaller (retry with halo_required, or 0 = no cull).
+     * <= 0: every particle is binned (no check needed).  k-NN interpolation entry points only. */
+    double slab_halo;
 } ptv_knn_params;
 
 /*
@@ -134,6 +144,9 @@ typedef struct {
     double ms_solve;     /* local RBF: the per-voxel solve kernels (ms_knn = their k-NN passes) */
     int64_t n_singular;  /* local RBF: voxels whose system had an exactly zero pivot */
     double ms_stencil;   /* ptv_divergence*: the stencil kernel */
+    int64_t n_binned;    /* particles binned (after the slab_halo cull; = n_particles without) */
+    double halo_required;/* slab_halo cull: the smallest halo this call proves exact (-1: no cull) */
+    double ms_cull;      /* slab_halo cull + exactness check (inside ms_bin / before ms_knn) */
 } ptv_stats;
 
 /*

@@ -248,8 +248,36 @@ def _poly(xhat, powers):
     return np.prod(xhat[..., None, :] ** powers, axis=-1)
 
 
+def solve_extended(lhs, rhs):
+    """Batched Gaussian elimination with partial pivoting in x87 extended precision
+    (``np.longdouble``, 64-bit significand) of float64 systems (C, m, m) x (C, m, S).
+
+    An accuracy reference, not the reference's algorithm: its error against the exact
+    solution of the float64 system is ~cond * 2^-64, about 2000x below that of a float64
+    LAPACK solve, so ``normwise(x_solver, x_extended)`` measures how far a float64 solver
+    (scipy's dgesv, numpy's, the GPU's) lands from the exact answer of the same system."""
+    A = np.array(lhs, dtype=np.longdouble)
+    B = np.array(rhs, dtype=np.longdouble)
+    C, m, _ = A.shape
+    ar = np.arange(C)
+    for c in range(m):
+        p = c + np.argmax(np.abs(A[:, c:, c]), axis=1)
+        if np.any(A[ar, p, c] == 0):
+            raise np.linalg.LinAlgError("Singular matrix")
+        A[:, [c], :], A[ar, p, :] = A[ar, p, :][:, None, :], A[:, c, :].copy()
+        B[:, [c], :], B[ar, p, :] = B[ar, p, :][:, None, :], B[:, c, :].copy()
+        l = A[:, c + 1:, c] / A[:, c, c][:, None]
+        A[:, c + 1:, c:] -= l[:, :, None] * A[:, c, c:][:, None, :]
+        B[:, c + 1:, :] -= l[:, :, None] * B[:, c, :][:, None, :]
+    X = np.empty_like(B)
+    for c in range(m - 1, -1, -1):
+        acc = B[:, c, :] - np.einsum("cj,cjs->cs", A[:, c, c + 1:], X[:, c + 1:, :])
+        X[:, c, :] = acc / A[:, c, c][:, None]
+    return X
+
+
 def rbf_local_points(points, values, queries, k, kernel="thin_plate_spline", epsilon=None, degree=None,
-                     smoothing=0.0, chunk=2048):
+                     smoothing=0.0, chunk=2048, solver="lapack"):
     """RBFInterpolator(points, values, neighbors=k, kernel, epsilon, degree, smoothing)(queries).
 
     Per query: KDTree k nearest (``_rbfinterp.py:513``), indices sorted ascending
@@ -300,12 +328,16 @@ def rbf_local_points(points, values, queries, k, kernel="thin_plate_spline", eps
         lhs[:, k:, :k] = np.swapaxes(P, 1, 2)
         rhs = np.zeros((len(ii), m, d.shape[1]))
         rhs[:, :k] = d[ii]
-        coeffs = np.linalg.solve(lhs, rhs)
         xq = x[c0:c0 + chunk]
         dq = xq[:, None, :] * epsilon - ye
         rq = np.sqrt((dq[..., 0] ** 2 + dq[..., 1] ** 2) + dq[..., 2] ** 2)
         vec = np.concatenate([phi(rq), _poly((xq - shift) / scale, powers)], axis=1)
-        out[c0:c0 + chunk] = np.einsum("qm,qms->qs", vec, coeffs)
+        if solver == "extended":
+            coeffs = solve_extended(lhs, rhs)
+            out[c0:c0 + chunk] = np.einsum("qm,qms->qs", vec.astype(np.longdouble), coeffs).astype(np.float64)
+        else:
+            coeffs = np.linalg.solve(lhs, rhs)
+            out[c0:c0 + chunk] = np.einsum("qm,qms->qs", vec, coeffs)
     return out
 
 
@@ -356,6 +388,51 @@ def interp_grid_parallel(points, values, ax, ay, az, method="idw", k=8, power=2.
             V[s - z0 : s - z0 + u.shape[0]] = v
             W[s - z0 : s - z0 + u.shape[0]] = w
     return U, V, W
+
+
+def lattice_axis(a, step=4):
+    """The library's coarse-lattice axis (ptv_api.cpp prepare / k_subsample): every `step`-th
+    value of `a` plus the last."""
+    a = np.asarray(a, dtype=np.float64)
+    n = len(a)
+    m = 1 if n <= 1 else (n - 1 + step - 1) // step + 1
+    return a[np.minimum(np.arange(m) * step, n - 1)]
+
+
+def slab_cull_interp(points, values, ax, ay, az, z0, z1, method="idw", k=8, power=2.0, halo=0.0):
+    """Restatement of the library's slab cull (ptv_knn_params.slab_halo) for the CPU tests of the
+    multi-GPU partition (tests/test_distributed.py): keep the particles with z within `halo` of
+    the slab's z extent (order kept), prove exactness from the lattice k-th distances D(c) of the
+    kept set (need(c) = D(c) + diag(c) + dz(c) - m(c), ptv_knn.hip k_halo_need, with exact D),
+    and interpolate planes [z0, z1) from the kept set.  Returns (U, V, W, halo_required,
+    n_kept); the interpolation is skipped (None) when halo_required > halo."""
+    from scipy.spatial import KDTree
+
+    P = np.asarray(points, dtype=np.float64)
+    Q = np.asarray(values, dtype=np.float64)
+    zs = np.asarray(az, dtype=np.float64)[z0:z1]
+    zmin, zmax = zs.min(), zs.max()
+    keep = (P[:, 2] >= zmin - halo) & (P[:, 2] <= zmax + halo)
+    Pk, Qk = P[keep], Q[keep]
+    lax, lay, laz = lattice_axis(ax), lattice_axis(ay), lattice_axis(zs)
+
+    def step(a):
+        d = np.abs(np.diff(a))
+        left = np.concatenate([[0.0], d])
+        right = np.concatenate([d, [0.0]])
+        return np.maximum(left, right)
+
+    Zc, Yc, Xc = np.meshgrid(laz, lay, lax, indexing="ij")
+    D, _ = KDTree(Pk).query(np.stack([Xc.ravel(), Yc.ravel(), Zc.ravel()], -1), k=k)
+    D = np.asarray(D).reshape(len(laz), len(lay), len(lax), -1)[..., -1]
+    sz, sy, sx = np.meshgrid(step(laz), step(lay), step(lax), indexing="ij")
+    diag = np.sqrt(sx ** 2 + sy ** 2 + sz ** 2)
+    m = np.maximum(np.minimum(Zc - zmin, zmax - Zc), 0.0)
+    required = float(max(np.max(D + diag + sz - m), 0.0))
+    if required > halo:
+        return None, None, None, required, int(keep.sum())
+    U, V, W = interp_grid(Pk, Qk, ax, ay, az, method, k, power, z0, z1)
+    return U, V, W, required, int(keep.sum())
 
 
 def nan_fill_and_mask(U, V, W, fluid_mask=None):

@@ -58,7 +58,7 @@ class Grid(C.Structure):
 class KnnParams(C.Structure):
     _fields_ = [("method", C.c_int), ("k", C.c_int), ("power", C.c_double), ("eps", C.c_double),
                 ("fluid_mask", C.POINTER(C.c_uint8)), ("flags", C.c_uint32), ("cell_occupancy", C.c_double),
-                ("r0_scale", C.c_double), ("lattice_bounds", C.c_int)]
+                ("r0_scale", C.c_double), ("lattice_bounds", C.c_int), ("slab_halo", C.c_double)]
 
 
 class RbfParams(C.Structure):
@@ -105,7 +105,8 @@ class Stats(C.Structure):
                 ("ms_total", C.c_double), ("n_particles", C.c_int64), ("n_voxels", C.c_int64),
                 ("n_cells", C.c_int64), ("cells", C.c_int32 * 3), ("cell_size", C.c_double * 3),
                 ("r0", C.c_double), ("ms_solve", C.c_double), ("n_singular", C.c_int64),
-                ("ms_stencil", C.c_double)]
+                ("ms_stencil", C.c_double), ("n_binned", C.c_int64), ("halo_required", C.c_double),
+                ("ms_cull", C.c_double)]
 
     def as_dict(self):
         d = {f: getattr(self, f) for f, _ in self._fields_}
@@ -177,6 +178,15 @@ def lib():
     return _lib
 
 
+class InexactError(PtvError):
+    """PTV_E_INEXACT: the slab_halo cull could not be proven exact (ptv_knn_params.slab_halo);
+    ``halo_required`` is the halo that would be."""
+
+    def __init__(self, code, msg, halo_required=None):
+        super().__init__(code, msg)
+        self.halo_required = halo_required
+
+
 def check(rc):
     if rc != PTV_OK:
         msg = lib().ptv_last_error().decode(errors="replace")
@@ -188,8 +198,16 @@ def check(rc):
             raise NotImplementedError(msg)
         if rc == PTV_E_SINGULAR:
             raise np.linalg.LinAlgError(msg)
+        if rc == PTV_E_INEXACT:
+            raise InexactError(rc, msg)
         raise PtvError(rc, msg)
     return rc
+
+
+def _check_knn(rc, st):
+    if rc == PTV_E_INEXACT:
+        raise InexactError(rc, lib().ptv_last_error().decode(errors="replace"), st.halo_required)
+    check(rc)
 
 
 def abi_sizes():
@@ -220,6 +238,17 @@ def as_dp(a: np.ndarray):
 
 def dev_dp(ptr: int):
     return C.cast(C.c_void_p(ptr), _dp)
+
+
+def _outputs(out, shape, dtype):
+    """Three output arrays: the caller's (checked: C-contiguous, shape, dtype) or new ones."""
+    if out is None:
+        return [np.empty(shape, dtype=dtype) for _ in range(3)]
+    out = list(out)
+    for a in out:
+        if a.shape != tuple(shape) or a.dtype != dtype or not a.flags.c_contiguous or not a.flags.writeable:
+            raise ValueError(f"out arrays must be writeable C-contiguous {dtype} of shape {tuple(shape)}")
+    return out
 
 
 def _flat_tiles(gp, shape, fluid_mask, z_range):
@@ -376,8 +405,11 @@ class Context:
     # -- host buffers ------------------------------------------------------
     def interp_knn(self, points, values, axes=None, grid_points=None, shape=None, method=METHOD_IDW, k=8,
                    power=2.0, eps=1e-10, fluid_mask=None, flags=0, z_range=None, cell_occupancy=0.0,
-                   r0_scale=0.0, lattice_bounds=0):
-        """Host-array k-NN interpolation. Returns (U, V, W) float64 (nz', ny, nx)."""
+                   r0_scale=0.0, lattice_bounds=0, slab_halo=0.0, out=None):
+        """Host-array k-NN interpolation. Returns (U, V, W) float64 (nz', ny, nx).
+
+        ``out``: optional three C-contiguous (nz', ny, nx) arrays of the output dtype (e.g.
+        z-slices of the caller's full arrays) written in place by the D2H."""
         pts = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 3)
         vals = np.ascontiguousarray(values, dtype=np.float64).reshape(-1, 3)
         cols = [np.ascontiguousarray(pts[:, i]) for i in range(3)] + [np.ascontiguousarray(vals[:, i]) for i in range(3)]
@@ -409,18 +441,19 @@ class Context:
             keep.append(mk)
         prm = KnnParams(method, int(k), float(power), float(eps),
                         mk.ctypes.data_as(C.POINTER(C.c_uint8)) if mk is not None else None, flags,
-                        float(cell_occupancy), float(r0_scale), int(lattice_bounds))
+                        float(cell_occupancy), float(r0_scale), int(lattice_bounds), float(slab_halo))
         odt = np.float32 if flags & FLAG_OUT_F32 else np.float64
-        out = [np.empty((z1 - z0, ny, nx), dtype=odt) for _ in range(3)]
+        out = _outputs(out, (z1 - z0, ny, nx), odt)
         st = Stats()
-        check(lib().ptv_interp_knn(self.h, C.byref(P), C.byref(G), C.byref(prm),
-                                   as_dp(out[0]), as_dp(out[1]), as_dp(out[2]), C.byref(st)))
+        rc = lib().ptv_interp_knn(self.h, C.byref(P), C.byref(G), C.byref(prm),
+                                  as_dp(out[0]), as_dp(out[1]), as_dp(out[2]), C.byref(st))
         self.stats = st.as_dict()
+        _check_knn(rc, st)
         return tuple(out)
 
     def interp_rbf(self, points, values, axes=None, grid_points=None, shape=None, k=20,
                    kernel="thin_plate_spline", epsilon=1.0, degree=1, smoothing=0.0, fluid_mask=None, flags=0,
-                   z_range=None, chunk_planes=0):
+                   z_range=None, chunk_planes=0, out=None):
         """Host-array local RBF (scipy RBFInterpolator(neighbors=k) semantics; the arguments are
         already resolved by ptv_interpolation_amd.rbf).  ``smoothing``: scalar or (n,) array.
         Returns (U, V, W) float64 (nz', ny, nx)."""
@@ -461,7 +494,7 @@ class Context:
                         as_dp(sm_arr) if sm_arr is not None else None,
                         mk.ctypes.data_as(C.POINTER(C.c_uint8)) if mk is not None else None, int(flags),
                         int(chunk_planes))
-        out = [np.empty((z1 - z0, ny, nx), dtype=np.float64) for _ in range(3)]
+        out = _outputs(out, (z1 - z0, ny, nx), np.float64)
         st = Stats()
         check(lib().ptv_interp_rbf_local(self.h, C.byref(P), C.byref(G), C.byref(prm),
                                          as_dp(out[0]), as_dp(out[1]), as_dp(out[2]), C.byref(st)))
@@ -492,7 +525,10 @@ class Context:
     # -- device buffers (integer device pointers, e.g. torch tensor data_ptr()) --
     def interp_knn_dev(self, n, pptrs, nx, ny, nz, axes_ptrs=None, point_ptrs=None, out_ptrs=None,
                        method=METHOD_IDW, k=8, power=2.0, eps=1e-10, mask_ptr=0, flags=0, z_range=None,
-                       stream=0, cell_occupancy=0.0, r0_scale=0.0, lattice_bounds=0):
+                       stream=0, cell_occupancy=0.0, r0_scale=0.0, lattice_bounds=0, slab_halo=0.0):
+        """Device-pointer k-NN interpolation (inputs resident in HBM), enqueued on `stream`;
+        returns the call's stats.  ``slab_halo`` > 0: see ptv_knn_params.slab_halo (raises
+        InexactError carrying ``halo_required`` when the halo is too small)."""
         P = Particles(int(n), *[dev_dp(p) for p in pptrs])
         if axes_ptrs is not None:
             G = Grid(nx, ny, nz, *[dev_dp(p) for p in axes_ptrs], None, None, None, 0, nz)
@@ -502,10 +538,11 @@ class Context:
         G.z_begin, G.z_end = z0, z1
         prm = KnnParams(method, int(k), float(power), float(eps),
                         C.cast(C.c_void_p(mask_ptr), C.POINTER(C.c_uint8)) if mask_ptr else None, flags,
-                        float(cell_occupancy), float(r0_scale), int(lattice_bounds))
+                        float(cell_occupancy), float(r0_scale), int(lattice_bounds), float(slab_halo))
         st = Stats()
-        check(lib().ptv_interp_knn_dev(self.h, C.byref(P), C.byref(G), C.byref(prm),
-                                       *[dev_dp(p) for p in out_ptrs], C.c_void_p(stream or 0), C.byref(st)))
+        rc = lib().ptv_interp_knn_dev(self.h, C.byref(P), C.byref(G), C.byref(prm),
+                                      *[dev_dp(p) for p in out_ptrs], C.c_void_p(stream or 0), C.byref(st))
+        _check_knn(rc, st)
         return st.as_dict()
 
     # -- consistent divergence (physics.py:6-53) ---------------------------

@@ -59,6 +59,8 @@ struct ptv_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev_knn0 = nullptr, ev_knn1 = nullptr, ev_bin0 = nullptr, ev_bin1 = nullptr, ev_lat1 = nullptr;
+    hipEvent_t ev_main0 = nullptr, ev_cull0 = nullptr, ev_cull1 = nullptr;  // main-kernel start; slab cull
+    bool cull_timed = false;
     bool timed_pending = false;
     DevBuf<double> pin[6], axes, qpts[3], out[3];
     DevBuf<uint8_t> mask;
@@ -81,11 +83,15 @@ struct ptv_ctx {
     DevBuf<uint8_t> flt_keep;                                    // outlier filter host calls
     DevBuf<uint32_t> flt_code, flt_perm, flt_count, flt_start, flt_scanp;  // filter: Morton keys/ids, sort temp
     DevBuf<double> flt_kth;
+    DevBuf<double> cull[6], cull_win;                            // slab cull: kept particles, z window
+    DevBuf<uint32_t> cull_cnt;                                   // slab cull: per-block counts
+    DevBuf<unsigned long long> halo_need;                        // slab cull: proven halo (double bits)
     hipEvent_t ev_div0 = nullptr, ev_div1 = nullptr;             // around the divergence stencil
     bool div_pending = false;
     std::vector<hipEvent_t> rbf_ev;                              // 3 per chunk: knn start, solve start, end
     int rbf_chunks = 0;
     double *h_bbox = nullptr;  // pinned, 6 doubles
+    unsigned long long *h_misc = nullptr;  // pinned scratch words (cull count, halo bound)
     ptv_stats last{};
 };
 
@@ -159,9 +165,13 @@ int ptv_init(int device, ptv_ctx **out) {
     PTV_HIP(hipEventCreate(&c->ev_bin0));
     PTV_HIP(hipEventCreate(&c->ev_bin1));
     PTV_HIP(hipEventCreate(&c->ev_lat1));
+    PTV_HIP(hipEventCreate(&c->ev_main0));
+    PTV_HIP(hipEventCreate(&c->ev_cull0));
+    PTV_HIP(hipEventCreate(&c->ev_cull1));
     PTV_HIP(hipEventCreate(&c->ev_div0));
     PTV_HIP(hipEventCreate(&c->ev_div1));
     PTV_HIP(hipHostMalloc(&c->h_bbox, 8 * sizeof(double)));
+    PTV_HIP(hipHostMalloc(&c->h_misc, 4 * sizeof(unsigned long long)));
     *out = c;
     return PTV_OK;
 }
@@ -205,6 +215,14 @@ int ptv_free(ptv_ctx *c) {
     c->flt_keep.release();
     for (auto *b : {&c->flt_code, &c->flt_perm, &c->flt_count, &c->flt_start, &c->flt_scanp}) b->release();
     c->flt_kth.release();
+    for (auto &b : c->cull) b.release();
+    c->cull_win.release();
+    c->cull_cnt.release();
+    c->halo_need.release();
+    if (c->h_misc) hipHostFree(c->h_misc);
+    hipEventDestroy(c->ev_main0);
+    hipEventDestroy(c->ev_cull0);
+    hipEventDestroy(c->ev_cull1);
     hipEventDestroy(c->ev_div0);
     hipEventDestroy(c->ev_div1);
     for (hipEvent_t e : c->rbf_ev) hipEventDestroy(e);
@@ -503,6 +521,7 @@ int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchP
         for (int d = 0; d < 3; ++d) kl.cb.n[d] = lat[0].n[d];
     }
     PTV_HIP(hipEventRecord(c->ev_lat1, s));
+    PTV_HIP(hipEventRecord(c->ev_main0, s));  // moved to the main launch when a check runs in between
 
     ptv_stats &ls = c->last;
     ls = ptv_stats{};
@@ -514,7 +533,19 @@ int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchP
         ls.cell_size[a] = cg.cs[a];
     }
     ls.r0 = kl.r0;
+    ls.n_binned = n;
+    ls.halo_required = -1.0;
     return PTV_OK;
+}
+
+// Whether prepare() will build the coarse lattice for planes [z0, z1) of a separable grid
+// (the same test as its loop's first iteration).
+bool lattice_built(const ptv_grid *g, int lattice_bounds) {
+    if (lattice_bounds < 0) return false;
+    const long long n[3] = {g->nx, g->ny, g->z_end - g->z_begin};
+    long long stop = kLatticeStopPoints;
+    if (const char *e = std::getenv("PTV_LAT_STOP")) stop = std::atoll(e);
+    return n[0] * n[1] * n[2] > stop && std::min(n[0], std::min(n[1], n[2])) >= 9;
 }
 
 SearchParams knn_search(const ptv_knn_params *prm) {
@@ -528,7 +559,58 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
     const SearchParams sp = knn_search(prm);
     KnnLaunch kl;
     Binned b{};
-    PTV_TRY(prepare(c, p, g, &sp, ax, ay, az, qx, qy, qz, s, kl, b));
+    // slab cull (ptv_knn_params.slab_halo): bin only the particles near this z-slab
+    ptv_particles pe = *p;
+    bool culled = false;
+    c->cull_timed = false;
+    if (prm->slab_halo > 0.0 && ax != nullptr && lattice_built(g, prm->lattice_bounds)) {
+        const int64_t n = p->n;
+        const size_t nb = cull_blocks(n);
+        for (auto &d : c->cull) PTV_TRY(d.ensure(n));
+        PTV_TRY(c->cull_win.ensure(4));
+        PTV_TRY(c->cull_cnt.ensure(nb + 1));
+        const double *src[6] = {p->x, p->y, p->z, p->u, p->v, p->w};
+        double *dst[6];
+        for (int a = 0; a < 6; ++a) dst[a] = c->cull[a].p;
+        uint32_t *h_total = reinterpret_cast<uint32_t *>(c->h_misc);
+        PTV_HIP(hipEventRecord(c->ev_cull0, s));
+        PTV_TRY(launch_cull(src, n, az, (int)g->z_begin, (int)g->z_end, prm->slab_halo, c->cull_win.p,
+                            c->cull_cnt.p, dst, h_total, s));
+        PTV_HIP(hipEventRecord(c->ev_cull1, s));
+        PTV_HIP(hipStreamSynchronize(s));
+        const int64_t kept = (int64_t)*h_total;
+        if (kept >= prm->k) {  // fewer than k could never be proven exact: bin everything
+            pe = ptv_particles{kept, dst[0], dst[1], dst[2], dst[3], dst[4], dst[5]};
+            culled = true;
+            c->cull_timed = true;
+        }
+    }
+    PTV_TRY(prepare(c, &pe, g, &sp, ax, ay, az, qx, qy, qz, s, kl, b));
+    if (culled) {
+        if (kl.cb.dk == nullptr) {
+            set_error("slab cull: no lattice bounds to prove exactness");
+            return PTV_E_INEXACT;
+        }
+        PTV_TRY(c->halo_need.ensure(1));
+        PTV_TRY(launch_halo_need(kl.cb.ax, kl.cb.ay, kl.cb.az, kl.cb.n[0], kl.cb.n[1], kl.cb.n[2], kl.cb.dk,
+                                 c->cull_win.p, kl.cg.mg, c->halo_need.p, s));
+        PTV_HIP(hipMemcpyAsync(c->h_misc + 1, c->halo_need.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+        PTV_HIP(hipStreamSynchronize(s));
+        double need;
+        std::memcpy(&need, &c->h_misc[1], sizeof(need));
+        c->last.n_particles = p->n;
+        c->last.n_binned = pe.n;
+        c->last.halo_required = need;
+        c->timed_pending = true;  // bin / lattice / cull timings of this call stay readable
+        if (!(need <= prm->slab_halo)) {
+            PTV_HIP(hipEventRecord(c->ev_main0, s));  // no main launch: empty kernel interval
+            PTV_HIP(hipEventRecord(c->ev_knn1, s));
+            set_error("slab cull not proven exact: slab_halo " + std::to_string(prm->slab_halo) +
+                      " < required " + std::to_string(need) + " (retry with >= halo_required, or 0)");
+            return PTV_E_INEXACT;
+        }
+        PTV_HIP(hipEventRecord(c->ev_main0, s));
+    }
     c->rbf_chunks = 0;
     PTV_TRY(launch_knn(kl, b, ax, ay, az, qx, qy, qz, mask, U, V, W, s));
     PTV_HIP(hipEventRecord(c->ev_knn1, s));
@@ -691,8 +773,14 @@ int finish_timing(ptv_ctx *c) {
         c->last.ms_solve = solve;
     } else {
         PTV_HIP(hipEventSynchronize(c->ev_knn1));
-        PTV_HIP(hipEventElapsedTime(&ms, c->ev_lat1, c->ev_knn1));
+        PTV_HIP(hipEventElapsedTime(&ms, c->ev_main0, c->ev_knn1));
         c->last.ms_knn = ms;
+    }
+    if (c->cull_timed) {
+        float a = 0.f, b = 0.f;
+        PTV_HIP(hipEventElapsedTime(&a, c->ev_cull0, c->ev_cull1));
+        PTV_HIP(hipEventElapsedTime(&b, c->ev_lat1, c->ev_main0));
+        c->last.ms_cull = (double)a + (double)b;
     }
     PTV_HIP(hipEventElapsedTime(&ms, c->ev_knn0, c->ev_lat1));
     c->last.ms_lattice = ms;

@@ -322,6 +322,125 @@ __global__ __launch_bounds__(256) void k_place(const uint32_t *__restrict__ inv,
     pval[s] = make_double4(u[i], v[i], w[i], 0.0);
 }
 
+// ---------------------------------------------------------------------------
+// slab cull (multi-GPU z-slab with replicated particles, ptv_knn_params.slab_halo):
+// keep the particles with z in [min(az[z0..z1)) - halo, max(az[z0..z1)) + halo], in their
+// original relative order (order-preserving compaction: per-block counts, scan, write)
+// ---------------------------------------------------------------------------
+constexpr int kCullItems = 16;
+constexpr int kCullTile = 256 * kCullItems;  // particles per block
+
+// win[0..3] = (zlo, zhi, slab z min, slab z max)
+__global__ __launch_bounds__(256) void k_slab_window(const double *__restrict__ az, int z0, int z1, double halo,
+                                                     double *__restrict__ win) {
+    double lo = INFINITY, hi = -INFINITY;
+    for (int i = z0 + (int)threadIdx.x; i < z1; i += 256) {
+        lo = fmin(lo, az[i]);
+        hi = fmax(hi, az[i]);
+    }
+    __shared__ double rl[256], rh[256];
+    rl[threadIdx.x] = lo;
+    rh[threadIdx.x] = hi;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) {
+            rl[threadIdx.x] = fmin(rl[threadIdx.x], rl[threadIdx.x + s]);
+            rh[threadIdx.x] = fmax(rh[threadIdx.x], rh[threadIdx.x + s]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        win[0] = rl[0] - halo;
+        win[1] = rh[0] + halo;
+        win[2] = rl[0];
+        win[3] = rh[0];
+    }
+}
+
+__device__ __forceinline__ bool in_window(double z, const double *win) { return z >= win[0] && z <= win[1]; }
+
+__global__ __launch_bounds__(256) void k_cull_count(const double *__restrict__ z, int64_t n,
+                                                    const double *__restrict__ win, uint32_t *__restrict__ bcount) {
+    const double lo = win[0], hi = win[1];
+    const int64_t base = (int64_t)blockIdx.x * kCullTile + threadIdx.x;
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < kCullItems; ++j) {
+        const int64_t i = base + (int64_t)j * 256;
+        if (i < n) {
+            const double v = z[i];
+            c += (v >= lo && v <= hi) ? 1u : 0u;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    __shared__ uint32_t ws[4];
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) bcount[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+struct Cols6 {
+    const double *src[6];
+    double *dst[6];
+};
+
+// item (j, thread) of a block is particle base + j*256 + thread: j-major, thread-minor is
+// index order, so the ranks below preserve it
+__global__ __launch_bounds__(256) void k_cull_write(Cols6 c, int64_t n, const double *__restrict__ win,
+                                                    const uint32_t *__restrict__ boff) {
+    const double lo = win[0], hi = win[1];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __shared__ uint32_t wcnt[kCullItems][4];
+    const int64_t base = (int64_t)blockIdx.x * kCullTile + threadIdx.x;
+    bool keep[kCullItems];
+#pragma unroll
+    for (int j = 0; j < kCullItems; ++j) {
+        const int64_t i = base + (int64_t)j * 256;
+        keep[j] = false;
+        if (i < n) {
+            const double v = c.src[2][i];
+            keep[j] = v >= lo && v <= hi;
+        }
+        const unsigned long long m = __builtin_amdgcn_ballot_w64(keep[j]);
+        if (lane == 0) wcnt[j][wid] = (uint32_t)__builtin_popcountll(m);
+    }
+    __syncthreads();
+    uint32_t off = boff[blockIdx.x];
+#pragma unroll
+    for (int j = 0; j < kCullItems; ++j) {
+        const unsigned long long m = __builtin_amdgcn_ballot_w64(keep[j]);
+        uint32_t pre = off;
+        for (int w = 0; w < wid; ++w) pre += wcnt[j][w];
+        if (keep[j]) {
+            const uint32_t r = pre + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+            const int64_t i = base + (int64_t)j * 256;
+#pragma unroll
+            for (int a = 0; a < 6; ++a) c.dst[a][r] = c.src[a][i];
+        }
+        off += wcnt[j][0] + wcnt[j][1] + wcnt[j][2] + wcnt[j][3];
+    }
+}
+
+size_t cull_blocks(int64_t n) { return (size_t)((n + kCullTile - 1) / kCullTile); }
+
+int launch_cull(const double *const src[6], int64_t n, const double *az, int z0, int z1, double halo, double *win,
+                uint32_t *bcount, double *const dst[6], uint32_t *h_total, hipStream_t s) {
+    const int nb = (int)cull_blocks(n);
+    hipLaunchKernelGGL(k_slab_window, dim3(1), dim3(256), 0, s, az, z0, z1, halo, win);
+    hipLaunchKernelGGL(k_cull_count, dim3(nb), dim3(256), 0, s, src[2], n, (const double *)win, bcount);
+    hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(1024), 0, s, bcount, nb);  // total -> bcount[nb]
+    Cols6 c;
+    for (int a = 0; a < 6; ++a) {
+        c.src[a] = src[a];
+        c.dst[a] = dst[a];
+    }
+    hipLaunchKernelGGL(k_cull_write, dim3(nb), dim3(256), 0, s, c, n, (const double *)win, (const uint32_t *)bcount);
+    PTV_HIP(hipGetLastError());
+    PTV_HIP(hipMemcpyAsync(h_total, bcount + nb, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    return PTV_OK;
+}
+
 int launch_bin(const CellGrid &cg, const double *const px[3], const double *const pv[3], int64_t n,
                uint32_t *d_code, uint32_t *d_perm, uint32_t *d_count, uint32_t *d_start,
                uint32_t *d_scan_partials, double4 *d_prec, double4 *d_pval, hipStream_t s) {

@@ -20,6 +20,13 @@ int launch_bin(const CellGrid &cg, const double *const px[3], const double *cons
 
 size_t scan_partials_needed(size_t m);
 
+// slab cull (ptv_knn_params.slab_halo): win (4 doubles) = (zlo, zhi, slab z min, slab z max),
+// bcount: cull_blocks(n) + 1 scratch words; the kept count is copied to the HOST word *h_total
+// (pinned; valid after the stream synchronises).  Order-preserving.
+size_t cull_blocks(int64_t n);
+int launch_cull(const double *const src[6], int64_t n, const double *az, int z0, int z1, double halo, double *win,
+                uint32_t *bcount, double *const dst[6], uint32_t *h_total, hipStream_t s);
+
 // ---- k-NN interpolation (ptv_knn.hip) ----
 // Exact k-th-neighbour distances on a coarser separable lattice (every `step`-th
 // point of this launch's grid, plus the last): d_k(v) <= dk(c) + |v - c| for any
@@ -62,6 +69,15 @@ int launch_count_bound(const CellGrid &g, const uint32_t *cstart, const double *
 
 // out[j] = in[min(step*j, n-1)] for j < nout (lattice axes)
 int launch_subsample(const double *in, int n, int step, double *out, int nout, hipStream_t s);
+
+// Smallest z halo that makes a slab-culled k-NN exact, from the finest lattice's k-th
+// distance bounds dk over (nx, ny, nz) lattice points with axes lax, lay, laz and the slab's
+// z extent win[2..3]: max over lattice points c of D(c) + diag(c) + dz(c) - m(c), where
+// diag(c) / dz(c) bound the adjacent lattice cells' diagonal / z extent and m(c) is c's
+// distance to the nearer slab face.  out: one u64 (max of non-negative doubles' bits),
+// zeroed by the launcher; mg: absolute margin.
+int launch_halo_need(const double *lax, const double *lay, const double *laz, int nx, int ny, int nz,
+                     const double *dk, const double *win, double mg, unsigned long long *out, hipStream_t s);
 
 int kmax_for(int k);  // compile-time list length serving k, 0 if unsupported
 extern unsigned long long *g_dbg;  // per-wave phase stamps (diagnostics), NULL = off

@@ -1029,6 +1029,52 @@ int launch_subsample(const double *in, int n, int step, double *out, int nout, h
     return PTV_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Exactness of a slab-culled particle set (ptv_knn_params.slab_halo).  For lattice point c
+// and any voxel v of a lattice cell with corner c: d_k(v) <= D(c) + |v - c| <= D(c) +
+// diag(c), and v's distance to the nearer slab face is >= m(c) - dz(c); a culled particle is
+// farther than halo + that distance.  So halo >= D(c) + diag(c) + dz(c) - m(c) for every c
+// proves every voxel's k nearest are inside the window (strictly nearer, so no tie either).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double axis_step(const double *a, int j, int n) {
+    // the larger of the two lattice intervals adjacent to point j (0 on a one-point axis)
+    const double l = j > 0 ? fabs(a[j] - a[j - 1]) : 0.0;
+    const double r = j + 1 < n ? fabs(a[j + 1] - a[j]) : 0.0;
+    return fmax(l, r);
+}
+
+__global__ __launch_bounds__(256) void k_halo_need(const double *__restrict__ lax, const double *__restrict__ lay,
+                                                   const double *__restrict__ laz, int nx, int ny, int nz,
+                                                   const double *__restrict__ dk, const double *__restrict__ win,
+                                                   double mg, unsigned long long *__restrict__ out) {
+    const long long np = (long long)nx * ny * nz;
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    double need = 0.0;
+    if (i < np) {
+        const int ix = (int)(i % nx), iy = (int)((i / nx) % ny), iz = (int)(i / ((long long)nx * ny));
+        const double sx = axis_step(lax, ix, nx), sy = axis_step(lay, iy, ny), sz = axis_step(laz, iz, nz);
+        const double diag = sqrt((sx * sx + sy * sy) + sz * sz);
+        const double zc = laz[iz];
+        const double m = fmax(fmin(zc - win[2], win[3] - zc), 0.0);
+        const double D = dk[i];
+        // rounding margin: relative 1e-9 on the distance terms plus the binning margin
+        need = fmax(((D + diag + sz) * (1.0 + 1e-9) + mg) - m * (1.0 - 1e-12), 0.0);
+        if (!(need < INFINITY)) need = INFINITY;
+    }
+    need = group_reduce<0x3f>(need, OpMax{});
+    if ((threadIdx.x & 63) == 0) atomicMax(out, (unsigned long long)__double_as_longlong(need));
+}
+
+int launch_halo_need(const double *lax, const double *lay, const double *laz, int nx, int ny, int nz,
+                     const double *dk, const double *win, double mg, unsigned long long *out, hipStream_t s) {
+    const long long np = (long long)nx * ny * nz;
+    PTV_HIP(hipMemsetAsync(out, 0, sizeof(unsigned long long), s));
+    hipLaunchKernelGGL(k_halo_need, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, s, lax, lay, laz, nx, ny, nz, dk,
+                       win, mg, out);
+    PTV_HIP(hipGetLastError());
+    return PTV_OK;
+}
+
 static const int kKmaxList[] = {4, 8, 12, 16, 24, 32, 40, 48, 56, 64};
 
 int kmax_for(int k) {

@@ -33,7 +33,7 @@
 // coordinates, r = sqrt((dx^2 + dy^2) + dz^2), monomials as products of integer
 // powers); elimination uses fused multiply-adds like the OpenBLAS dger kernels.  The
 // factorisation order differs from LAPACK's blocked dgetrf, so results agree with the
-// reference to the conditioning of the system (see tests/test_rbf.py and DESIGN.md).
+// reference to the conditioning of the system (see tests/test_gpu_rbf.py and DESIGN.md).
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
@@ -45,13 +45,23 @@
 namespace ptv {
 
 // 1/p from v_rcp_f64 and two Newton steps (within an ulp of the IEEE quotient; the
-// elimination multiplier l = a * (1/p) is LAPACK dgetf2's reciprocal scaling anyway)
+// elimination multiplier l = a * (1/p) is LAPACK dgetf2's reciprocal scaling anyway).
+// Valid only where 1/p is a normal number: see elim_multiplier.
 __device__ __forceinline__ double rcp_nr(double p) {
     double r = __builtin_amdgcn_rcp(p);
     double e = fma(-p, r, 1.0);
     r = fma(r, e, r);
     e = fma(-p, r, 1.0);
     return fma(r, e, r);
+}
+
+// l = a / p as LAPACK dgetf2 forms it: a * (1/p) when |p| >= sfmin (DBL_MIN), a / p below.
+// The Newton reciprocal serves 2^-1020 < |p| < 2^1020; outside it (an infinite pivot gives
+// rcp 0 and fma(-inf, 0, 1) = NaN; a subnormal one overflows the seed) the IEEE forms run.
+__device__ __forceinline__ double elim_multiplier(double a, double p) {
+    const double ap = fabs(p);
+    if (ap > 0x1p-1020 && ap < 0x1p1020) return a * rcp_nr(p);
+    return ap >= DBL_MIN ? a * (1.0 / p) : a / p;
 }
 
 __device__ __forceinline__ void rbf_wave_sync() {
@@ -378,7 +388,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M <= 32 ? 3
         const double piv = prow_buf[c];
         const bool upd = !done && !isP;
         if (upd && pos == c) pos = (int)prow_buf[M + 3];  // the swap moves this row to the pivot's position
-        const double l = (upd && piv != 0.0) ? A[c] * rcp_nr(piv) : 0.0;
+        const double l = (upd && piv != 0.0) ? elim_multiplier(A[c], piv) : 0.0;
 #pragma unroll
         for (int j = c + 1; j < M; ++j) A[j] = fma(-l, prow_buf[j], A[j]);
         b0 = fma(-l, prow_buf[M], b0);

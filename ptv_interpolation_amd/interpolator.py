@@ -178,12 +178,15 @@ def separable_axes(X, Y, Z):
     ay = np.ascontiguousarray(Y[0, :, 0], dtype=np.float64)
     az = np.ascontiguousarray(Z[:, 0, 0], dtype=np.float64)
 
-    def fits(A, ref):
-        if A.strides.count(0) == 2:  # zero-stride broadcast view (create_grid(dense=False))
+    def fits(A, ref, axis):
+        # zero-stride broadcast view (create_grid(dense=False)): constant along the two other
+        # axes by construction, provided the one nonzero stride sits on `axis`
+        st = A.strides
+        if all(st[d] == 0 for d in range(3) if d != axis):
             return True
         return np.array_equal(A, np.broadcast_to(ref, A.shape))
 
-    if fits(X, ax[None, None, :]) and fits(Y, ay[None, :, None]) and fits(Z, az[:, None, None]):
+    if fits(X, ax[None, None, :], 2) and fits(Y, ay[None, :, None], 1) and fits(Z, az[:, None, None], 0):
         return ax, ay, az
     return None
 
@@ -212,8 +215,9 @@ def _knn_field(points, values, grid_tuple, method, k, power):
     axes = separable_axes(X, Y, Z)
     if axes is not None:
         # z-slab per device (launcher.py); bit-identical to one whole-grid call
-        U, V, W = launcher.run_slabs(len(axes[2]), lambda ctx, z0, z1: ctx.interp_knn(
-            points, values, axes=axes, method=m, k=k, power=power, eps=_EPS, z_range=(z0, z1)))
+        full = [np.empty((len(axes[2]), len(axes[1]), len(axes[0]))) for _ in range(3)]
+        U, V, W = launcher.run_slabs(len(axes[2]), lambda ctx, z0, z1, views: ctx.interp_knn(
+            points, values, axes=axes, method=m, k=k, power=power, eps=_EPS, z_range=(z0, z1), out=views), full)
     else:
         ctx = _lib.Context.get(launcher.devices()[0])
         size = int(np.prod(shape))

@@ -52,20 +52,28 @@ def context(device: int, slot: int) -> "_lib.Context":
     return c
 
 
-def run_slabs(nz: int, fn):
-    """fn(ctx, z0, z1) -> tuple of (z1 - z0, ...) arrays; returns their z concatenation.
+def run_slabs(nz: int, fn, out):
+    """Fill the preallocated C-contiguous (nz, ...) arrays ``out`` slab by slab.
 
-    One slab per device of ``devices()``; a single device runs fn(ctx, 0, nz) directly."""
+    ``fn(ctx, z0, z1, views)`` writes planes [z0, z1) into ``views`` (the z-slices of ``out``,
+    contiguous, written in place by the library's D2H: no per-slab arrays and no host
+    concatenation).  One slab per device of ``devices()``, one host thread each; a single
+    device runs fn(ctx, 0, nz, out) directly.  Returns ``out``."""
+    out = tuple(out)
+    for a in out:
+        if not (a.flags.c_contiguous and a.shape[0] == nz):
+            raise ValueError("run_slabs: outputs must be C-contiguous with nz leading planes")
     devs = devices()
     if len(devs) <= 1 or nz < 2:
-        return fn(_lib.Context.get(devs[0]), 0, nz)
+        fn(_lib.Context.get(devs[0]), 0, nz, out)
+        return out
     slabs = slab_bounds(nz, len(devs))
     seen = {}
     jobs = []
     for d, (z0, z1) in zip(devs, slabs):
         slot = seen.get(d, 0)
         seen[d] = slot + 1
-        jobs.append((context(d, slot), z0, z1))
+        jobs.append((context(d, slot), z0, z1, tuple(a[z0:z1] for a in out)))
     with ThreadPoolExecutor(len(jobs)) as ex:
-        parts = list(ex.map(lambda j: fn(*j), jobs))
-    return tuple(np.concatenate([p[c] for p in parts], axis=0) for c in range(len(parts[0])))
+        list(ex.map(lambda j: fn(*j), jobs))
+    return out

@@ -13,11 +13,9 @@ path (SURVEY.md §8(f) names only the divergence).
 """
 from __future__ import annotations
 
-import os
-
 import numpy as np
 
-from . import _lib
+from . import _lib, launcher
 
 __all__ = ["compute_consistent_divergence"]
 
@@ -52,7 +50,7 @@ def compute_consistent_divergence(u, v, w, mask, dx, dy, dz):
         raise NotImplementedError("spacings that promote float32 fields differently per axis "
                                   f"({sorted(map(str, rts))}) are not supported on the GPU path")
     rt = rts.pop()
-    ctx = _lib.Context.get(int(os.environ.get("PTV_DEVICE", "0")))
+    ctx = _lib.Context.get(launcher.devices()[0])  # PTV_DEVICE, else the first of PTV_DEVICES / all
     return ctx.divergence(u.astype(ft, copy=False), v.astype(ft, copy=False), w.astype(ft, copy=False),
                           np.asarray(mask).astype(bool, copy=False), float(dx), float(dy), float(dz),
                           result_dtype=rt)

@@ -123,12 +123,14 @@ class LocalRBFInterpolator:
             g[:, : min(3, S - c0)] = self.d[:, c0:c0 + 3]
             yield c0, min(3, S - c0), g
 
-    def _run(self, ctx=None, **grid):
+    def _run(self, ctx=None, out=None, **grid):
+        """``out``: optional three arrays for a three-component evaluation, written in place."""
         ctx = ctx if ctx is not None else _lib.Context.get(_device())
         outs = []
         for c0, w, g in self._groups():
             res = ctx.interp_rbf(self.y, g, k=self.neighbors, kernel=self.kernel, epsilon=self.epsilon,
-                                 degree=self.degree, smoothing=self.smoothing, **grid)
+                                 degree=self.degree, smoothing=self.smoothing,
+                                 out=out if self.d.shape[1] == 3 else None, **grid)
             self.stats = ctx.stats
             outs.extend(res[:w])
         return outs
@@ -147,10 +149,11 @@ class LocalRBFInterpolator:
         out = np.stack([c.reshape(-1) for c in comps], axis=-1)
         return out.reshape((nx,) + self.d_shape)
 
-    def evaluate_grid(self, ax, ay, az, fluid_mask=None, flags=0, z_range=None, ctx=None):
+    def evaluate_grid(self, ax, ay, az, fluid_mask=None, flags=0, z_range=None, ctx=None, out=None):
         """Evaluate on the separable grid meshgrid(az, ay, ax, 'ij') (create_grid axes) without
-        materialising the (V, 3) query list; returns one (nz', ny, nx) array per component."""
-        return self._run(ctx=ctx, axes=(ax, ay, az), fluid_mask=fluid_mask, flags=flags, z_range=z_range)
+        materialising the (V, 3) query list; returns one (nz', ny, nx) array per component
+        (``out``: three preallocated arrays for three components, filled in place)."""
+        return self._run(ctx=ctx, out=out, axes=(ax, ay, az), fluid_mask=fluid_mask, flags=flags, z_range=z_range)
 
 
 def rbf_field(points, values, grid_tuple, k, kernel, smoothing, n_jobs=1):
@@ -174,8 +177,11 @@ def rbf_field(points, values, grid_tuple, k, kernel, smoothing, n_jobs=1):
         from . import launcher
 
         # z-slab per device (launcher.py), as interpolator.py:173-182 fans out over processes
-        U, V, W = launcher.run_slabs(len(axes[2]), lambda ctx, z0, z1: tuple(
-            interp.evaluate_grid(*axes, z_range=(z0, z1), ctx=ctx)))
+        if interp.d.shape[1] != 3:
+            raise ValueError("interpolate_field values must have three components (u, v, w)")
+        full = [np.empty((len(axes[2]), len(axes[1]), len(axes[0]))) for _ in range(3)]
+        U, V, W = launcher.run_slabs(len(axes[2]), lambda ctx, z0, z1, views: interp.evaluate_grid(
+            *axes, z_range=(z0, z1), ctx=ctx, out=views), full)
     else:
         flat = np.stack([np.ravel(X), np.ravel(Y), np.ravel(Z)], axis=-1)
         out = interp(flat)

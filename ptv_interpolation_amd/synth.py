@@ -90,3 +90,23 @@ def fluid_mask(grid: int | tuple) -> np.ndarray:
     ax = [LO[i] + np.arange(g) * (HI[i] - LO[i]) / (g - 1) for i, g in enumerate((gx, gy, gz))]
     # broadcast views (same elementwise arithmetic as a meshgrid, no 3 x 8 B/voxel temporaries)
     return ~inside_spheres(ax[0][None, None, :], ax[1][None, :, None], ax[2][:, None, None])
+
+
+def fluid_mask_device(grid: int | tuple, z0: int, z1: int, device):
+    """Planes [z0, z1) of ``fluid_mask(grid)`` as a torch uint8 (z1 - z0, gy, gx) tensor built
+    on `device` (plane z is copy-local plane z % gz: stacked copies repeat the pack), with the
+    same float64 arithmetic as ``fluid_mask`` (bit-identical; no (gz, gy, gx) float64 host
+    temporaries, which reach 69 GB at 2048^3)."""
+    import torch
+
+    gx, gy, gz = (grid, grid, grid) if isinstance(grid, int) else grid
+    f64 = dict(dtype=torch.float64, device=device)
+    ax = [float(LO[i]) + (torch.arange(g, **f64) * float(HI[i] - LO[i])) / float(g - 1)
+          for i, g in enumerate((gx, gy, gz))]
+    x = ax[0][None, None, :]
+    y = ax[1][None, :, None]
+    z = ax[2][torch.arange(z0, z1, device=device) % gz][:, None, None]
+    inside = torch.zeros((z1 - z0, gy, gx), dtype=torch.bool, device=device)
+    for cx, cy, cz in CENTERS:
+        inside |= ((x - float(cx)) ** 2 + (y - float(cy)) ** 2 + (z - float(cz)) ** 2) < R * R
+    return (~inside).to(torch.uint8)

@@ -1,0 +1,114 @@
+"""Multi-GPU z-slab partition of ONE grid with the particle set replicated (SURVEY.md §8(e),
+BASELINE north_star; replaces the reference's process fan-out, interpolator.py:173-182).
+
+One process per GPU.  Rank r of P computes planes ``slab_bounds(nz, P)[r]`` of the grid.
+Every rank holds the whole particle set in HBM (replicated once with an RCCL all-gather or
+broadcast, outside the timed step) and the library bins only the particles within
+``slab_halo`` of its slab (``ptv_knn_params.slab_halo``: on-device compaction, then a proof
+from the coarse-lattice k-th distance bounds that no culled particle can be among any slab
+voxel's k nearest).  When the proof fails the call returns ``PTV_E_INEXACT`` with the halo it
+would have needed; ``interp_slab`` retries with that halo (a superset of the particles can only
+lower the bound, so one retry suffices) and, as a last resort, bins everything.  No collective
+touches the interpolation itself; an all-gather reassembles the full field only when a caller
+wants it on every device (``gather_field``).
+
+The functions take torch tensors / a ``torch.distributed`` module, so the same partition code
+runs over RCCL on the GPUs (bench.py) and over gloo on the CPU (tests/test_distributed.py,
+with an oracle-backed ``call``).
+"""
+from __future__ import annotations
+
+import math
+
+from . import _lib
+from .launcher import slab_bounds
+
+__all__ = ["rank_slab", "halo_slab", "replicate_columns", "broadcast_columns", "HaloState", "interp_slab",
+           "halo_guess", "gather_field"]
+
+
+def rank_slab(nz: int, world: int, rank: int):
+    """[z0, z1) planes of rank `rank` (contiguous, as even as possible, in rank order)."""
+    return slab_bounds(nz, world)[rank] if rank < min(world, nz) else (nz, nz)
+
+
+def halo_slab(z0: int, z1: int, nz: int, planes: int = 1):
+    """The slab grown by `planes` halo planes per interior side, clipped to the grid, and the
+    (lo, hi) number of halo planes added (a stencil's one-plane halo, physics.py:6-53)."""
+    a, b = max(0, z0 - planes), min(nz, z1 + planes)
+    return a, b, z0 - a, b - z1
+
+
+def replicate_columns(local, dist=None):
+    """All-gather each rank's equal-length 1-D column tensors into the replicated columns
+    (rank order).  ``local``: list of tensors; returns a list of tensors."""
+    if dist is None or dist.get_world_size() == 1:
+        return list(local)
+    out = []
+    for c in local:
+        full = c.new_empty((dist.get_world_size() * c.numel(),))
+        dist.all_gather_into_tensor(full, c.contiguous())
+        out.append(full)
+    return out
+
+
+def broadcast_columns(cols, dist=None, src: int = 0):
+    """Broadcast rank `src`'s column tensors in place (every rank allocated the same shapes)."""
+    if dist is not None and dist.get_world_size() > 1:
+        for c in cols:
+            dist.broadcast(c, src)
+    return cols
+
+
+class HaloState:
+    """The halo a rank uses for its slab cull; ``interp_slab`` widens it to the proven value."""
+
+    def __init__(self, halo: float):
+        self.halo = float(halo)
+        self.retries = 0
+        self.required = None
+
+    def as_dict(self):
+        return {"halo": self.halo, "required": self.required, "retries": self.retries}
+
+
+def interp_slab(call, state: HaloState, max_tries: int = 3):
+    """``call(halo) -> stats dict`` (a ``Context.interp_knn_dev`` bound to this rank's slab);
+    on ``InexactError`` retry with the halo the library proved sufficient, last resort 0 (every
+    particle binned, nothing to prove)."""
+    for _ in range(max_tries):
+        try:
+            st = call(state.halo)
+            state.required = st.get("halo_required")
+            return st
+        except _lib.InexactError as e:
+            state.retries += 1
+            h = e.halo_required
+            state.halo = h * (1.0 + 1e-6) if (h is not None and math.isfinite(h) and h > 0) else 0.0
+            if state.halo == 0.0:
+                break
+    state.halo = 0.0
+    st = call(0.0)
+    state.required = None
+    return st
+
+
+def halo_guess(n_particles: int, extent, k: int, factor: float = 4.0) -> float:
+    """First halo to try: `factor` x the radius of a ball holding k particles at the mean
+    density over `extent` (x, y, z lengths)."""
+    vol = 1.0
+    for e in extent:
+        vol *= max(float(e), 1e-300)
+    r = (k * vol / (max(n_particles, 1) * 4.18879020478639)) ** (1.0 / 3.0)
+    return factor * r
+
+
+def gather_field(slab, dist=None):
+    """All-gather the ranks' equal-size (planes, ny, nx) slabs into the (world * planes, ny, nx)
+    field on every rank (RCCL over xGMI on the GPUs): the reassembly step, never on the data
+    path of the interpolation."""
+    if dist is None or dist.get_world_size() == 1:
+        return slab
+    full = slab.new_empty((dist.get_world_size() * slab.shape[0],) + tuple(slab.shape[1:]))
+    dist.all_gather_into_tensor(full, slab.contiguous())
+    return full

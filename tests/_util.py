@@ -50,3 +50,19 @@ def boundary_ties(points, ax, ay, az, k):
     if kk <= k:
         return np.zeros(X.shape, bool)
     return (d[:, k - 1] == d[:, k]).reshape(X.shape)
+
+
+def filter_ties(points, k):
+    """(n,) bool: particles whose remove_outliers_knn decision depends on cKDTree's tie order.
+
+    The reference drops column 0 of ``KDTree.query(points, k + 1)`` (filtering.py:26-30) as
+    "the point itself"; with a coincident twin that column may be the twin (a different
+    speed).  A tie between the (k+1)-th and (k+2)-th neighbour distances changes the
+    neighbour set.  Either makes the keep decision traversal dependent."""
+    from scipy.spatial import KDTree
+
+    P = np.asarray(points, dtype=np.float64)
+    d, _ = KDTree(P).query(P, k=min(k + 2, len(P)))
+    twin = d[:, 1] == 0.0
+    tie = d[:, k] == d[:, k + 1] if d.shape[1] > k + 1 else np.zeros(len(P), bool)
+    return twin | tie

@@ -298,10 +298,69 @@ def filter_cases(ref_path):
               stdout=np.array(buf.getvalue()))
 
 
+def filter_dup_case(ref_path):
+    """remove_outliers_knn with coincident particles (duplicated positions, different
+    velocities): cKDTree's column 0 of query(k+1) (filtering.py:26-30) is then any of the
+    coincident points, traversal dependent, so the keep mask of those points and of
+    particles whose (k+1)-th / (k+2)-th neighbours tie is tie-dependent (the tests exclude
+    them, tests/test_gpu_mask_filter.py)."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("ref_filtering", os.path.join(ref_path, "filtering.py"))
+    filtering = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(filtering)
+    rng = np.random.default_rng(57)
+    n = 3000
+    P = rng.uniform(0, 15, (n, 3))
+    src = rng.choice(n, 200, replace=False)
+    dst = rng.choice(np.setdiff1d(np.arange(n), src), 200, replace=False)
+    P[dst] = P[src]                                   # 200 coincident pairs
+    P[dst[:20]] = P[src[0]]                           # and one 21-fold cluster
+    Q = np.stack([np.sin(P[:, 0] / 3), np.cos(P[:, 1] / 4), 0.1 * P[:, 2]], 1) + 0.05 * rng.standard_normal((n, 3))
+    Q[dst[::7]] *= 6.0                                # twins with outlying velocities
+    k, thr = 10, 3.0
+    df = _df(P, Q)
+    df["id"] = np.arange(n)
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        out = filtering.remove_outliers_knn(df, k=k, threshold=thr)
+    keep = np.zeros(n, dtype=bool)
+    keep[out["id"].values] = True
+    _save(f"filter_dup_k{k}_t{thr}", points=P, values=Q, k=k, threshold=thr, keep=keep, stdout=np.array(buf.getvalue()))
+
+
+def rbf_truth_cases():
+    """Accuracy reference for the ill-conditioned Gaussian fixtures (cond up to 6e8): the same
+    float64 systems solved in extended precision (oracle.cpu_ref.solve_extended).  Stores the
+    exact-answer field plus how far the two CPU LAPACK paths land from it (scipy's dgesv =
+    the golden U, V, W; numpy's batched gesv = the oracle), so the GPU bound in
+    tests/test_gpu_rbf.py is the reference's own distance to the exact answer."""
+    sys.path.insert(0, os.path.join(HERE, "..", ".."))
+    from oracle import cpu_ref
+
+    for deg in (0, -1):
+        name = f"rbf_gaussian_eps0.3_k32_deg{deg}"
+        g = np.load(os.path.join(HERE, name + ".npz"))
+        q = cpu_ref.grid_queries(g["ax"], g["ay"], g["az"])
+        ext = cpu_ref.rbf_local_points(g["points"], g["values"], q, 32, "gaussian", 0.3, deg, solver="extended")
+        npl = cpu_ref.rbf_local_points(g["points"], g["values"], q, 32, "gaussian", 0.3, deg)
+        shape = g["U"].shape
+        truth = [np.ascontiguousarray(ext[:, c].reshape(shape)) for c in range(3)]
+
+        def nw(a, b):
+            return float(np.max(np.abs(a - b)) / np.max(np.abs(b)))
+
+        gap_scipy = [nw(g[c], t) for c, t in zip("UVW", truth)]
+        gap_numpy = [nw(npl[:, i].reshape(shape), t) for i, t in enumerate(truth)]
+        _save("truth_" + name, U=truth[0], V=truth[1], W=truth[2], gap_scipy=np.array(gap_scipy),
+              gap_numpy=np.array(gap_numpy))
+        print("  scipy-vs-exact", gap_scipy, "numpy-vs-exact", gap_numpy)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
-    ap.add_argument("--only", default="knn,edge,masked,rbf,nearest,div,mask,filter")
+    ap.add_argument("--only", default="knn,edge,masked,rbf,nearest,div,mask,filter,filterdup,rbftruth")
     a = ap.parse_args()
     ref = _import_reference(a.ref)
     only = a.only.split(",")
@@ -321,6 +380,10 @@ def main():
         mask_cases(ref)
     if "filter" in only:
         filter_cases(a.ref)
+    if "filterdup" in only:
+        filter_dup_case(a.ref)
+    if "rbftruth" in only:
+        rbf_truth_cases()
 
 
 if __name__ == "__main__":

@@ -17,7 +17,7 @@ import pandas as pd
 import pytest
 
 from oracle import cpu_ref
-from tests._util import load, names
+from tests._util import filter_ties, load, names
 
 pytestmark = pytest.mark.gpu
 
@@ -148,8 +148,16 @@ def test_outlier_filter_golden(ctx, name):
         out = filtering.remove_outliers_knn(df, k=int(g["k"]), threshold=float(g["threshold"]))
     keep = np.zeros(len(df), dtype=bool)
     keep[out["id"].values] = True
-    assert np.array_equal(keep, g["keep"])
-    assert buf.getvalue() == str(g["stdout"])
+    ties = filter_ties(g["points"], int(g["k"]))
+    if ties.any():
+        # coincident particles (filter_dup_*): the tie-dependent decisions are excluded, the
+        # rest must match; the radius line is tie-independent
+        assert name.startswith("filter_dup"), "unexpected ties in a continuous fixture"
+        assert np.array_equal(keep[~ties], g["keep"][~ties])
+        assert buf.getvalue().splitlines()[0] == str(g["stdout"]).splitlines()[0]
+    else:
+        assert np.array_equal(keep, g["keep"])
+        assert buf.getvalue() == str(g["stdout"])
     assert list(out.index) == list(range(len(out)))  # reset_index(drop=True)
 
 

@@ -22,6 +22,7 @@ pytestmark = pytest.mark.gpu
 
 TOL = 1e-10
 TOL_ILL = 1e-8
+TRUTH_FACTOR = 2.0  # GPU distance to the exact answer vs the CPU LAPACKs' (see the Gaussian test)
 
 
 @pytest.fixture(scope="module")
@@ -64,16 +65,31 @@ def test_golden_dropin(ctx, name, capsys):
 
 @pytest.mark.parametrize("name", [n for n in names(("rbf",)) if "gaussian" in n])
 def test_golden_gaussian_scipy_oracle(ctx, name):
-    """RBFInterpolator(kernel='gaussian', epsilon=0.3, degree=0/-1) — scipy oracle cases."""
+    """RBFInterpolator(kernel='gaussian', epsilon=0.3, degree=0/-1) — scipy oracle cases.
+
+    These systems have cond up to 6e8, and no float64 solver reaches the 1e-10 bar on them:
+    tests/golden/make_golden.py (rbf_truth_cases) solved the same float64 systems in
+    extended precision and measured scipy's own dgesv result (the golden U, V, W) 0.8e-9 to
+    2.4e-9 normwise away from that exact answer, numpy's LAPACK 1.0e-9 to 1.7e-9
+    (``gap_scipy`` / ``gap_numpy`` in truth_<name>.npz).  The bar for the GPU is therefore
+    the reference's own accuracy: its distance to the exact answer must stay within
+    TRUTH_FACTOR x the worse of the two CPU LAPACK distances, per component (and within
+    TOL_ILL of scipy's result).  The achieved errors are printed (pytest -s / the log)."""
     from ptv_interpolation_amd.rbf import LocalRBFInterpolator
 
     g = load(name)
+    t = load("truth_" + name)
     it = LocalRBFInterpolator(g["points"], g["values"], neighbors=int(g["k"]), kernel="gaussian",
                               epsilon=float(g["epsilon"]), degree=int(g["degree"]),
                               smoothing=float(g["smoothing"]))
     U, V, W = it.evaluate_grid(g["ax"], g["ay"], g["az"])
-    for a, b in ((U, g["U"]), (V, g["V"]), (W, g["W"])):
-        assert normwise(a, b) <= TOL_ILL
+    for i, (c, a) in enumerate(zip("UVW", (U, V, W))):
+        e_ref, e_exact = normwise(a, g[c]), normwise(a, t[c])
+        gap = max(float(t["gap_scipy"][i]), float(t["gap_numpy"][i]))
+        print(f"{name} {c}: gpu-vs-scipy {e_ref:.3e}  gpu-vs-exact {e_exact:.3e}  "
+              f"scipy-vs-exact {float(t['gap_scipy'][i]):.3e}  numpy-vs-exact {float(t['gap_numpy'][i]):.3e}")
+        assert e_exact <= max(TOL, TRUTH_FACTOR * gap)
+        assert e_ref <= TOL_ILL
 
 
 def _rand_case(seed, n, G, lo=0.0, hi=None):
@@ -198,3 +214,47 @@ def test_full_size_sampled(ctx):
     ref = cpu_ref.rbf_local_points(P, Q, q, 32, "thin_plate_spline")
     for c, a in enumerate((U, V, W)):
         assert normwise(a.ravel()[sel], ref[:, c]) <= TOL
+
+
+def test_extreme_pivots_take_the_ieee_path(ctx):
+    """Pivots outside the v_rcp_f64 + Newton range (|p| >= 2^1020: smoothing 1e308 on some
+    diagonals) take LAPACK dgetf2's IEEE reciprocal; results stay finite and match the oracle."""
+    from oracle import cpu_ref
+    from ptv_interpolation_amd.rbf import LocalRBFInterpolator
+
+    P, Q, ax = _rand_case(61, 3000, 10)
+    sm = np.zeros(len(P))
+    sm[::5] = 1e308
+    U, V, W = LocalRBFInterpolator(P, Q, neighbors=20, smoothing=sm).evaluate_grid(ax, ax, ax)
+    ref = cpu_ref.rbf_local_grid(P, Q, ax, ax, ax, 20, smoothing=sm)
+    for a, b in zip((U, V, W), ref):
+        assert np.isfinite(a).all()
+        assert normwise(a, b) <= TOL
+
+
+def test_c3_full_size_gaussian_sampled(ctx):
+    """C3 (BASELINE configs[2]): 512^3 grid, 5M sphere-pack particles, local Gaussian RBF
+    eps = 0.3, degree -1 (32 x 32 systems), k = 32, the whole grid on the GPU, 3000 random
+    voxels against the oracle (scipy KDTree + LAPACK gesv per voxel) and against the exact
+    answer of the same systems (extended precision).  Bar: gpu-vs-exact within
+    max(1e-10, TRUTH_FACTOR x lapack-vs-exact); the achieved errors are printed."""
+    from oracle import cpu_ref
+    from ptv_interpolation_amd import synth
+    from ptv_interpolation_amd.rbf import LocalRBFInterpolator
+
+    G = 512
+    P, Q = synth.sphere_pack(5_000_000, G, values="normal")
+    ax = np.linspace(0, G - 1, G)
+    it = LocalRBFInterpolator(P, Q, neighbors=32, kernel="gaussian", epsilon=0.3, degree=-1)
+    out = it.evaluate_grid(ax, ax, ax)
+    rng = np.random.default_rng(2024)
+    sel = rng.integers(0, G ** 3, 3000)
+    iz, iy, ix = np.unravel_index(sel, (G, G, G))
+    q = np.stack([ax[ix], ax[iy], ax[iz]], -1)
+    lap = cpu_ref.rbf_local_points(P, Q, q, 32, "gaussian", 0.3, -1)
+    ext = cpu_ref.rbf_local_points(P, Q, q, 32, "gaussian", 0.3, -1, solver="extended")
+    for c, a in enumerate(out):
+        got = a.ravel()[sel]
+        e_ref, e_exact, gap = normwise(got, lap[:, c]), normwise(got, ext[:, c]), normwise(lap[:, c], ext[:, c])
+        print(f"C3 {'UVW'[c]}: gpu-vs-lapack {e_ref:.3e}  gpu-vs-exact {e_exact:.3e}  lapack-vs-exact {gap:.3e}")
+        assert e_exact <= max(TOL, TRUTH_FACTOR * gap)

@@ -34,6 +34,10 @@ def test_separable_axes_detection():
     X2 = X.copy(); X2[1, 2, 3] += 0.5
     assert ip.separable_axes(X2, Y, Z) is None
     assert ip.separable_axes(X.ravel(), Y.ravel(), Z.ravel()) is None
+    # a zero-stride view varying along the WRONG axis (x values along z) is not separable
+    (Xc, Yc, Zc), (xc, _, _) = ip.create_grid(((0, 5), (0, 5), (0, 5)), 5, dense=False)
+    assert ip.separable_axes(Xc, Yc, Zc) is not None
+    assert ip.separable_axes(np.broadcast_to(xc[:, None, None], Xc.shape), Yc, Zc) is None
 
 
 def _df(n=20, seed=0):
