@@ -605,6 +605,7 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
         if (!(need <= prm->slab_halo)) {
             PTV_HIP(hipEventRecord(c->ev_main0, s));  // no main launch: empty kernel interval
             PTV_HIP(hipEventRecord(c->ev_knn1, s));
+            if (st) *st = c->last;  // halo_required for the caller's retry
             set_error("slab cull not proven exact: slab_halo " + std::to_string(prm->slab_halo) +
                       " < required " + std::to_string(need) + " (retry with >= halo_required, or 0)");
             return PTV_E_INEXACT;

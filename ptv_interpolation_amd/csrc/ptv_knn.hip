@@ -71,6 +71,7 @@ struct KnnKernelArgs {
     int lz0;           // plane of coarse-lattice point 0
     uint32_t *slots;   // kModeSlots: neighbour slots out
     int seed_n;        // seed records used per lattice corner (<= k)
+    int nblocks;       // workgroups of the launch (the grid may be 2-D, see launch_knn)
 };
 
 // numpy pairwise sum of a[0..n) (n <= KMAX <= 128), from identity 0.0.
@@ -322,7 +323,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
     // XCD-aware block order: the dispatcher deals workgroups round-robin over the 8 XCDs,
     // so give XCD x a contiguous range of tiles (neighbouring tiles share cell rows and
     // particle records; each XCD has its own L2)
-    const int b = xcd_block(blockIdx.x, gridDim.x);
+    const int lb = (int)(blockIdx.y * gridDim.x + blockIdx.x);  // linear dispatch order
+    if (lb >= a.nblocks) return;                                  // 2-D grid padding (block-uniform)
+    const int b = xcd_block(lb, a.nblocks);
     const int bx = b % a.ntxb;
     const int rr = b / a.ntxb;
     const int ty = rr % a.nty;
@@ -922,7 +925,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
     store_out(a.flags, U, V, W, vo, out[0], out[1], out[2]);
     if constexpr (STAMP) {
         stamp(t_epi);
-        const long long gw = (long long)blockIdx.x * 4 + wid;
+        const long long gw = (long long)lb * 4 + wid;
         if (dbg != nullptr && gw < dbg_cap && (threadIdx.x & 63) == (int)__builtin_ffsll((long long)__builtin_amdgcn_ballot_w64(true)) - 1) {
             unsigned long long *r = dbg + gw * kStampFields;
             r[0] = t_setup;
@@ -1148,7 +1151,12 @@ int launch_knn(const KnnLaunch &a, const Binned &b, const double *ax, const doub
         set_error("grid too large for one launch");
         return PTV_E_ARG;
     }
-    dim3 grid((unsigned)nblocks);
+    // a dispatch holds < 2^32 work-items per dimension: above 2^23 blocks of 256 the grid is
+    // 2-D, x a multiple of 8 so that the linear order still deals blocks round-robin over XCDs
+    constexpr long long kMaxGridX = 1LL << 23;
+    ka.nblocks = (int)nblocks;
+    dim3 grid(nblocks <= kMaxGridX ? (unsigned)nblocks : (unsigned)kMaxGridX,
+              nblocks <= kMaxGridX ? 1u : (unsigned)((nblocks + kMaxGridX - 1) / kMaxGridX));
     switch (km) {
 #define PTV_CASE(K) \
     case K: launch_t<K>(grid, s, ka, b, ax, ay, az, qx, qy, qz, mask, U, V, W); break;

@@ -171,6 +171,7 @@ def test_c5_rank_share_f32_and_divergence(ctx):
     zslab.interp_slab(call, state)
     assert ctx.last_stats()["n_binned"] < n
     mask = synth.fluid_mask_device(G, za, zb, torch.device("cuda", 0))
+    torch.cuda.synchronize()  # the mask comes from torch's stream, the divergence runs on the context's
     div = torch.empty((z1 - z0, G, G), dtype=torch.float32, device="cuda")
     ctx.divergence_dev(G, G, zb - za, [o.data_ptr() for o in out], mask.data_ptr(), div.data_ptr(), 1.0, 1.0, 1.0,
                        field_dtype=_lib.F32, result_dtype=_lib.F32, z_range=(hlo, hlo + (z1 - z0)),
