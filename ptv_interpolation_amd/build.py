@@ -27,6 +27,13 @@ EXTRA = {"ptv_rbf.hip": ["-mllvm", "-pragma-unroll-threshold=1000000"]}
 
 COMMON = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", f"--offload-arch={ARCH}",
           "-I", INCLUDE, "-I", CSRC, "-Wno-unused-result"]
+# dev A/B builds: PTV_EXTRA_FLAGS="-DPTV_KNN_WAVES=5" PTV_BUILD_TAG=w5 builds ab/libptv_w5.so
+# (own object directory) without touching the shipped library
+EXTRA_FLAGS = os.environ.get("PTV_EXTRA_FLAGS", "").split()
+TAG = os.environ.get("PTV_BUILD_TAG", "")
+if TAG:
+    LIB = os.path.join(os.path.dirname(HERE), "ab", f"libptv_{TAG}.so")
+    BUILD = os.path.join(HERE, "csrc", "_build_" + TAG)
 
 
 def hipcc() -> str:
@@ -45,6 +52,7 @@ def _stale(obj: str, deps) -> bool:
 
 def build(verbose: bool = False, force: bool = False) -> str:
     os.makedirs(BUILD, exist_ok=True)
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
     cc = hipcc()
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h"))]
     headers.append(os.path.join(INCLUDE, "ptv_api.h"))
@@ -55,8 +63,8 @@ def build(verbose: bool = False, force: bool = False) -> str:
         obj = os.path.join(BUILD, src + ".o")
         objs.append(obj)
         if force or _stale(obj, [sp, __file__] + headers):
-            lang = ["-x", "hip"] if src.endswith(".hip") else ["-x", "hip"]
-            jobs.append([cc, *COMMON, *EXTRA.get(src, []), *lang, "-c", sp, "-o", obj])
+            lang = ["-x", "hip"]
+            jobs.append([cc, *COMMON, *EXTRA_FLAGS, *EXTRA.get(src, []), *lang, "-c", sp, "-o", obj])
 
     def run(cmd):
         if verbose:

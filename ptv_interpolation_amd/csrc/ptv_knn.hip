@@ -44,6 +44,13 @@
 
 namespace ptv {
 
+#ifndef PTV_SUBBALL_RUNS
+#define PTV_SUBBALL_RUNS 1  // clip the gather runs to the sub-balls' chords (0: the tile ball's)
+#endif
+#ifndef PTV_KNN_WAVES
+#define PTV_KNN_WAVES 4  // waves per SIMD the k <= 8 kernels are register-capped for
+#endif
+
 constexpr int kStampFields = 8;
 constexpr int kCap = 128;        // LDS candidate slots per wave (16 B fp32 + 32 B fp64 each)
 constexpr int kRowsPerLane = 1;  // cell rows examined per lane per gather round
@@ -292,7 +299,7 @@ __device__ __forceinline__ double axis_gap(int c, double o, double cs, double lo
 }
 
 template <int KMAX, bool STAMP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ? 4 : 1))) void k_knn_interp(KnnKernelArgs a, const double4 *__restrict__ prec,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ? PTV_KNN_WAVES : 1))) void k_knn_interp(KnnKernelArgs a, const double4 *__restrict__ prec,
                                                     const double4 *__restrict__ pval,
                                                     const uint32_t *__restrict__ cstart,
                                                     const double *__restrict__ ax, const double *__restrict__ ay,
@@ -666,6 +673,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
                                 hi2 = b1;
                             }
                             // both runs' bounds in flight together (an empty run reads cell 0 twice)
+#if PTV_SUBBALL_RUNS
+                            {
+                                // clip the runs to the union of the 8 sub-balls' chords of this row: a
+                                // particle that can enter any list lies in some sub-ball (the copy filter
+                                // below), so cells outside every chord are never needed.  fp32 on
+                                // tile-relative coordinates, every rounding widened (em).
+                                const float em = (float)(Mpass * 1e-6) + 1e-6f;
+                                const float ylo = (float)(g.o[1] + (double)ccy * g.cs[1] - tcy) - em;
+                                const float yhi = (float)(g.o[1] + (double)(ccy + 1) * g.cs[1] - tcy) + em;
+                                const float zlo = (float)(g.o[2] + (double)ccz * g.cs[2] - tcz) - em;
+                                const float zhi = (float)(g.o[2] + (double)(ccz + 1) * g.cs[2] - tcz) + em;
+                                float xl = INFINITY, xh = -INFINITY;
+#pragma unroll
+                                for (int sb = 0; sb < 8; ++sb) {
+                                    const float cyv = sby[(sb >> 1) & 1], czv = sbz[sb >> 2];
+                                    const float gy = fmaxf(fmaxf(ylo - cyv, cyv - yhi), 0.f);
+                                    const float gz = fmaxf(fmaxf(zlo - czv, czv - zhi), 0.f);
+                                    const float h2s = __fmaf_rn(gz, gz, gy * gy);
+                                    if (h2s <= sbr2[sb]) {
+                                        const float hw = sqrtf_up(fmaxf(sbr2[sb] - h2s, 0.f) + sbr2[sb] * 1e-6f);
+                                        xl = fminf(xl, sbx[sb & 1] - hw);
+                                        xh = fmaxf(xh, sbx[sb & 1] + hw);
+                                    }
+                                }
+                                if (xl <= xh) {
+                                    const int s0 = clampi(floor((tcx + (double)(xl - em) - g.o[0]) * g.ic[0]), g.nc[0]);
+                                    const int s1 = clampi(floor((tcx + (double)(xh + em) - g.o[0]) * g.ic[0]), g.nc[0]);
+                                    lo1 = max(lo1, s0);
+                                    hi1 = min(hi1, s1);
+                                    lo2 = max(lo2, s0);
+                                    hi2 = min(hi2, s1);
+                                } else {
+                                    hi1 = lo1 - 1;
+                                    hi2 = lo2 - 1;
+                                }
+                            }
+#endif
                             const uint32_t *rp = cstart + ((long long)ccz * g.nc[1] + ccy) * g.nc[0];
                             const bool e1 = lo1 <= hi1, e2 = lo2 <= hi2;
                             const uint32_t s1 = rp[e1 ? lo1 : 0], t1 = rp[e1 ? hi1 + 1 : 0];
