@@ -244,7 +244,11 @@ namespace {
 // particles per binning cell: the k <= 8 kernels (seeded, sub-ball filtered copy) are fastest
 // with coarse cells (fewer, longer runs per row: 512^3 / 5M k=8 main launch 19.1 -> 16.5 ms
 // from 1.2 to 5.5); the larger-k kernels prefer fine cells (k=50: 477 ms at 1.2, 493 at 5.5)
-constexpr double kDefaultOccupancySmallK = 5.5;
+// measured on the 512^3 / 5M sphere pack, k = 8 (tools/void_split.py, round 2): per-cell
+// occupancy 16 / 12 with cells 12x thinner along x (16 particles per x-column of 12 cells)
+// gave k-NN 14.9 ms against 16.3 ms for cubic cells of 5.5, the lattice 2.31 against 2.44
+constexpr double kDefaultOccupancySmallK = 16.0;  // particles per (y, z) cell column segment
+constexpr double kDefaultXRefSmallK = 12.0;       // x-refinement of the k <= 8 cells
 constexpr double kDefaultOccupancy = 1.2;
 constexpr double kDefaultR0Scale = 1.0;     // first gather radius / expected k-NN radius
 constexpr long long kMaxCells = 1LL << 28;
@@ -301,7 +305,7 @@ int validate_knn(const ptv_particles *p, const ptv_knn_params *prm) {
 }
 
 // Cell grid over the union bounding box: ~`occ` particles per cell on average.
-CellGrid make_cell_grid(const double lo_in[3], const double hi_in[3], int64_t n, double occ) {
+CellGrid make_cell_grid(const double lo_in[3], const double hi_in[3], int64_t n, double occ, double xref_in) {
     CellGrid cg{};
     double ext[3];
     double maxext = 0.0, maxabs = 0.0;
@@ -321,11 +325,18 @@ CellGrid make_cell_grid(const double lo_in[3], const double hi_in[3], int64_t n,
             ++dims;
         }
     double cs = dims ? std::pow(occ * vol / (double)n, 1.0 / dims) : 1.0;
+    // x-refinement: cells `xref` times thinner along x (occupancy / xref per cell).  A gather
+    // run is a contiguous x-range of cells whose cost is its two cstart loads whatever its
+    // length, so thin x-cells trim the runs' ends (fewer candidates outside the sub-balls)
+    // without adding rows.
+    double xref = std::max(1.0, xref_in);
+    if (const char *e = std::getenv("PTV_CELL_XREF")) xref = std::max(1.0, std::atof(e));  // dev override
     for (int iter = 0; iter < 64; ++iter) {  // cap the cell count (memory) by growing cs
         long long tot = 1;
         for (int a = 0; a < 3; ++a) {
             int nc = 1;
-            if (ext[a] > 1e-9 * maxext && cs > 0.0) nc = (int)std::max(1.0, std::min(1e6, std::ceil(ext[a] / cs)));
+            const double csa = a == 0 ? cs / xref : cs;
+            if (ext[a] > 1e-9 * maxext && csa > 0.0) nc = (int)std::max(1.0, std::min(1e6, std::ceil(ext[a] / csa)));
             cg.nc[a] = nc;
             tot *= nc;
         }
@@ -413,11 +424,12 @@ int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchP
     }
 
     // 2. binning
+    const bool small_k = kmax_for(prm->k) <= 8;
     const double occ = prm->cell_occupancy > 0.0 ? prm->cell_occupancy
-                       : (kmax_for(prm->k) <= 8 ? kDefaultOccupancySmallK : kDefaultOccupancy);
-    CellGrid cg = make_cell_grid(lo, hi, n, occ);
+                       : (small_k ? kDefaultOccupancySmallK : kDefaultOccupancy);
+    CellGrid cg = make_cell_grid(lo, hi, n, occ, small_k && !(prm->cell_occupancy > 0.0) ? kDefaultXRefSmallK : 1.0);
     const size_t m = (size_t)cg.ncells;
-    PTV_TRY(c->code.ensure(n));
+    PTV_TRY(c->code.ensure(2 * (size_t)n));  // cell codes + in-cell ranks (launch_bin)
     PTV_TRY(c->perm.ensure(n));
     PTV_TRY(c->prec.ensure(n));
     PTV_TRY(c->pval.ensure(n));

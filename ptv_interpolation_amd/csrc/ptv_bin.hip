@@ -133,10 +133,13 @@ __device__ __forceinline__ int cell_coord(double v, double o, double ic, int nc)
     return c;
 }
 
+// cell code + histogram; the atomic's return value is the particle's arrival rank in its
+// cell (any order: k_seg_sort makes the in-cell order deterministic), so the scatter needs no
+// second round of atomics
 __global__ __launch_bounds__(256) void k_cell_code(CellGrid cg, const double *__restrict__ x,
                                                    const double *__restrict__ y, const double *__restrict__ z,
                                                    int64_t n, uint32_t *__restrict__ code,
-                                                   uint32_t *__restrict__ count) {
+                                                   uint32_t *__restrict__ count, uint32_t *__restrict__ rank) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     int cx = cell_coord(x[i], cg.o[0], cg.ic[0], cg.nc[0]);
@@ -144,7 +147,7 @@ __global__ __launch_bounds__(256) void k_cell_code(CellGrid cg, const double *__
     int cz = cell_coord(z[i], cg.o[2], cg.ic[2], cg.nc[2]);
     uint32_t c = (uint32_t)(((long long)cz * cg.nc[1] + cy) * cg.nc[0] + cx);
     code[i] = c;
-    atomicAdd(&count[c], 1u);
+    rank[i] = atomicAdd(&count[c], 1u);
 }
 
 // ---------------------------------------------------------------------------
@@ -250,13 +253,11 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_final(const uint32_t *__r
 // scatter + deterministic in-cell order
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_scatter(const uint32_t *__restrict__ code, int64_t n,
-                                                 const uint32_t *__restrict__ start, uint32_t *__restrict__ fill,
-                                                 uint32_t *__restrict__ perm) {
+                                                 const uint32_t *__restrict__ start,
+                                                 const uint32_t *__restrict__ rank, uint32_t *__restrict__ perm) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    uint32_t c = code[i];
-    uint32_t slot = start[c] + atomicSub(&fill[c], 1u) - 1u;
-    perm[slot] = (uint32_t)i;
+    perm[start[code[i]] + rank[i]] = (uint32_t)i;
 }
 
 __device__ void sift_down(uint32_t *a, int root, int n) {
@@ -447,7 +448,8 @@ int launch_bin(const CellGrid &cg, const double *const px[3], const double *cons
     const size_t m = (size_t)cg.ncells;
     PTV_HIP(hipMemsetAsync(d_count, 0, m * sizeof(uint32_t), s));
     const int nb = (int)((n + 255) / 256);
-    hipLaunchKernelGGL(k_cell_code, dim3(nb), dim3(256), 0, s, cg, px[0], px[1], px[2], n, d_code, d_count);
+    uint32_t *d_rank = d_code + n;  // in-cell arrival ranks: the second half of the code buffer (2n)
+    hipLaunchKernelGGL(k_cell_code, dim3(nb), dim3(256), 0, s, cg, px[0], px[1], px[2], n, d_code, d_count, d_rank);
     const int sb = (int)((m + kScanTile - 1) / kScanTile);
     hipLaunchKernelGGL(k_scan_reduce, dim3(sb), dim3(kScanThreads), 0, s, (const uint32_t *)d_count, m,
                        d_scan_partials);
@@ -455,7 +457,7 @@ int launch_bin(const CellGrid &cg, const double *const px[3], const double *cons
     hipLaunchKernelGGL(k_scan_final, dim3(sb), dim3(kScanThreads), 0, s, (const uint32_t *)d_count, m,
                        (const uint32_t *)d_scan_partials, sb, d_start);
     hipLaunchKernelGGL(k_scatter, dim3(nb), dim3(256), 0, s, (const uint32_t *)d_code, n,
-                       (const uint32_t *)d_start, d_count, d_perm);
+                       (const uint32_t *)d_start, (const uint32_t *)d_rank, d_perm);
     // d_code is dead after the scatter: it holds the inverse permutation from here on
     hipLaunchKernelGGL(k_seg_sort, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, (const uint32_t *)d_start, m,
                        d_perm, d_code);

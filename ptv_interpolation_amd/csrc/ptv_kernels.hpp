@@ -13,7 +13,7 @@ int launch_bbox(const double *const px[3], int64_t n, const double *const qa[3],
 
 // Counting-sort the particles into linear-order cells (deterministic order
 // inside each cell: ascending original index).  Scratch buffers must hold
-// n entries (code, perm) and ncells (+1) entries (count, start).
+// 2n (code), n (perm) and ncells (+1) entries (count, start).
 int launch_bin(const CellGrid &cg, const double *const px[3], const double *const pv[3], int64_t n,
                uint32_t *d_code, uint32_t *d_perm, uint32_t *d_count, uint32_t *d_start,
                uint32_t *d_scan_partials, double4 *d_prec, double4 *d_pval, hipStream_t s);

@@ -21,9 +21,11 @@ fl = float(synth.fluid_mask(min(G, 256)).mean())
 rng = np.random.default_rng(3)
 Pu = rng.uniform(-0.5, G - 0.5, (int(N / fl), 3))
 occs = [float(x) for x in os.environ.get("OCCS", "0").split(",")]
-for occ, (name, PP) in [(o, c) for o in occs for c in (("spherepack", P), ("uniform", Pu))]:
+xrefs = [float(x) for x in os.environ.get("XREFS", "1").split(",")]
+for occ, xref, (name, PP) in [(o, x, c) for o in occs for x in xrefs for c in (("spherepack", P),)]:
     if occ > 0:
         os.environ["PTV_CELL_OCC"] = str(occ)
+    os.environ["PTV_CELL_XREF"] = str(xref)
     cols = [torch.from_numpy(np.ascontiguousarray(PP[:, i])).cuda() for i in range(3)] + \
            [torch.ones(len(PP), dtype=torch.float64, device="cuda") for _ in range(3)]
     acc = []
@@ -34,4 +36,4 @@ for occ, (name, PP) in [(o, c) for o in occs for c in (("spherepack", P), ("unif
         if it >= 2:
             acc.append((st["ms_bin"], st["ms_lattice"], st["ms_knn"]))
     b, l, kk = np.mean(acc, axis=0)
-    print(f"occ {occ} {name:11s} n {len(PP)} bin {b:.3f} lattice {l:.3f} knn {kk:.3f} ms  cells {st['cells']}", flush=True)
+    print(f"occ {occ} xref {xref} {name:11s} n {len(PP)} bin {b:.3f} lattice {l:.3f} knn {kk:.3f} ms  cells {st['cells']}", flush=True)
