@@ -69,7 +69,7 @@ struct ptv_ctx {
     DevBuf<double> bbox_part, bbox_out;
     DevBuf<unsigned long long> dbg;
     DevBuf<double> lat_axes[kMaxLattice], lat_dk[kMaxLattice];  // coarse-lattice bound levels
-    DevBuf<double4> lat_recs[kMaxLattice];                       // their k-NN records (seeds)
+    DevBuf<float4> lat_recs[kMaxLattice];                        // their k-NN records (seeds, fp32 relative)
     DevBuf<uint32_t> slots;                                      // local RBF: chunk k-NN slots
     DevBuf<int> rbf_pw, rbf_status;                              // monomial exponents, singular count
     DevBuf<double> smooth;                                       // per-particle smoothing (host calls)
@@ -447,7 +447,7 @@ int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchP
     struct Lat {
         int n[3];
         double *ax, *ay, *az, *dk;
-        double4 *recs;  // NULL on the coarsest (count-bound) level and for k > 8
+        float4 *recs;   // NULL on the coarsest (count-bound) level and for k > 8
     };
     Lat lat[kMaxLattice];
     int nlat = 0;

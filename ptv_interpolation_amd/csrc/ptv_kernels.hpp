@@ -37,7 +37,7 @@ constexpr int kLatticeStep = 1 << kLatticeShift;
 struct CoarseBound {
     const double *ax = nullptr, *ay = nullptr, *az = nullptr;  // lattice axes
     const double *dk = nullptr;                                // (n[2], n[1], n[0]) k-th distances
-    const double4 *recs = nullptr;  // (n[2], n[1], n[0], k) k-NN particle records {x,y,z,slot}, or NULL
+    const float4 *recs = nullptr;   // (n[2], n[1], n[0], k) k-NN seed records {p - c (fp32), slot}, or NULL
     int n[3] = {0, 0, 0};
 };
 
@@ -57,7 +57,7 @@ struct KnnLaunch {
     double r0;           // first gather radius (from the mean particle density)
     int mode = kModeInterp;
     CoarseBound cb;
-    double4 *kd_recs = nullptr;  // kModeKDist: also write each point's k-NN records here
+    float4 *kd_recs = nullptr;   // kModeKDist: also write each point's k-NN seed records here
     int lz0 = -1;                // plane of lattice point 0 (-1: z0); chunked launches keep the slab's
     uint32_t *slots = nullptr;   // kModeSlots: (z1 - z0, ny, nx, k) neighbour slots out
 };

@@ -74,7 +74,7 @@ struct KnnKernelArgs {
     double rall;  // radius that covers the whole cell grid from any query
     int mode;     // kModeInterp / kModeKDist
     CoarseBound cb;
-    double4 *kd_recs;  // kModeKDist: k-NN particle records out (NULL = none)
+    float4 *kd_recs;   // kModeKDist: k-NN seed records out (NULL = none): {p - c (fp32), slot}
     int lz0;           // plane of coarse-lattice point 0
     uint32_t *slots;   // kModeSlots: neighbour slots out
     int seed_n;        // seed records used per lattice corner (<= k)
@@ -356,10 +356,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
         qz = qpz[vfull];
     }
     const bool active = valid && (mask == nullptr || mask[vfull] != 0);
-    // seed records (k-NN lists of the tile's 8 lattice corners: lane = corner * 8 + entry, each a
-    // copy {x, y, z, slot} of the particle record), issued first so that their latency overlaps
-    // the lattice-bound loads below
-    double4 seed = make_double4(0.0, 0.0, 0.0, __longlong_as_double(-1LL));
+    // seed records (k-NN lists of the tile's 8 lattice corners: lane = corner * 8 + entry, each
+    // {particle - corner in fp32, slot}, 16 B), issued first so that their latency overlaps the
+    // lattice-bound loads below
+    float4 seed = make_float4(0.f, 0.f, 0.f, __uint_as_float(0xffffffffu));
+    double scx = 0.0, scy = 0.0, scz = 0.0;  // the lane's corner
     if constexpr (KMAX <= 8) {
         if (a.cb.recs != nullptr) {
             const int jx0 = __builtin_amdgcn_readfirstlane(cx >> kLatticeShift);
@@ -370,6 +371,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
             const int jy = min(jy0 + ((cc >> 1) & 1), a.cb.n[1] - 1);
             const int jz = min(jz0 + (cc >> 2), a.cb.n[2] - 1);
             if (j < a.seed_n) seed = a.cb.recs[(((size_t)jz * a.cb.n[1] + jy) * a.cb.n[0] + jx) * a.k + j];
+            scx = a.cb.ax[jx];
+            scy = a.cb.ay[jy];
+            scz = a.cb.az[jz];
         }
     }
 
@@ -452,8 +456,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
                 // back.  Equal slots -> one survivor; distinct slots that collide -> one survivor
                 // too, which only drops a seed: any subset of k distinct particles still bounds.
                 uint32_t *tab = reinterpret_cast<uint32_t *>(buf);
-                const uint32_t sl = (uint32_t)__double_as_longlong(seed.w);
-                const bool has = __double_as_longlong(seed.w) >= 0;
+                const uint32_t sl = __float_as_uint(seed.w);
+                const bool has = sl != 0xffffffffu;
                 const uint32_t hsh = (sl * 2654435761u) >> 22;  // 1024 entries = the 4 KB buffer
                 if (has) tab[hsh] = (uint32_t)lane;
                 wave_lds_sync();
@@ -463,13 +467,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
                 const int pos = __builtin_amdgcn_mbcnt_hi((unsigned)(um >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)um, 0u));
                 double pm = 0.0;
                 if (uniq) {
-                    const double ex = seed.x - tcx, ey = seed.y - tcy, ez = seed.z - tcz;
-                    fbx[pos] = (float)ex;
-                    fby[pos] = (float)ey;
-                    fbz[pos] = (float)ez;
-                    pm = fabs(ex) + fabs(ey) + fabs(ez);  // >= the Euclidean distance to the centre
+                    // particle - tile centre = (particle - corner) + (corner - centre): three fp32
+                    // roundings of magnitude <= Ms (covered by dl below)
+                    const float ex = seed.x + (float)(scx - tcx), ey = seed.y + (float)(scy - tcy),
+                                ez = seed.z + (float)(scz - tcz);
+                    fbx[pos] = ex;
+                    fby[pos] = ey;
+                    fbz[pos] = ez;
+                    // >= the Euclidean distance to the centre (fp32 sum rounded up)
+                    pm = ((double)fabsf(ex) + (double)fabsf(ey) + (double)fabsf(ez)) * (1.0 + 1e-6);
                 }
-                // seed-voxel distances are <= Ms; fp32 distance error <= Ms * 2^-21 (as cpass below)
+                // seed-voxel distances are <= Ms; fp32 coordinate + distance error <= Ms * 2^-19
                 const double Ms = uniform(wave_max(pm)) + bhalf;
                 wave_lds_sync();
                 float sd[KMAX];
@@ -496,7 +504,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
                 for (int q = 1; q < KMAX; ++q)
                     if (q == a.k - 1) kth = sd[q];
                 if (active && kth < INFINITY) {
-                    const double dl = Ms * 4.76837158203125e-07;
+                    const double dl = Ms * 1.9073486328125e-06;
                     const double st2 = ((double)kth * (1.0 + 9.5367431640625e-07) + (2.0 * Ms * dl + dl * dl)) * (1.0 + 1e-12);
                     if (st2 < ub2) {
                         ub2 = st2;
@@ -835,8 +843,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
     if (a.mode == kModeKDist) {
         U[vo] = sqrt(bd[KMAX - 1]);
         if (a.kd_recs != nullptr) {
-            // the k-NN records (list order) seed the next finer level's tiles
-            double4 *o = a.kd_recs + vo * (size_t)a.k;
+            // the k-NN records (list order) seed the next finer level's tiles: {p - this lattice
+            // point in fp32, slot}
+            float4 *o = a.kd_recs + vo * (size_t)a.k;
             double4 rec[KMAX];
 #pragma unroll
             for (int j = 0; j < KMAX; ++j) rec[j] = prec[max(bp[j], 0)];  // every load in flight at once
@@ -844,8 +853,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
             for (int j = 0; j < KMAX; ++j) {
                 if (j >= a.kpad) {
                     const bool ok = bp[j] >= 0;
-                    o[j - a.kpad] = make_double4(ok ? rec[j].x : 0.0, ok ? rec[j].y : 0.0, ok ? rec[j].z : 0.0,
-                                                 __longlong_as_double((long long)bp[j]));
+                    o[j - a.kpad] = make_float4(ok ? (float)(rec[j].x - qx) : 0.f, ok ? (float)(rec[j].y - qy) : 0.f,
+                                                ok ? (float)(rec[j].z - qz) : 0.f,
+                                                __uint_as_float(ok ? (uint32_t)bp[j] : 0xffffffffu));
                 }
             }
         }
