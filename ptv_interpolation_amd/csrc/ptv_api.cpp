@@ -70,6 +70,7 @@ struct ptv_ctx {
     DevBuf<unsigned long long> dbg;
     DevBuf<double> lat_axes[kMaxLattice], lat_dk[kMaxLattice];  // coarse-lattice bound levels
     DevBuf<float4> lat_recs[kMaxLattice];                        // their k-NN records (seeds, fp32 relative)
+    DevBuf<int> lat_order[kMaxLattice];                          // longest-first block order per level
     DevBuf<uint32_t> slots;                                      // local RBF: chunk k-NN slots
     DevBuf<int> rbf_pw, rbf_status;                              // monomial exponents, singular count
     DevBuf<double> smooth;                                       // per-particle smoothing (host calls)
@@ -199,6 +200,7 @@ int ptv_free(ptv_ctx *c) {
     for (auto &b : c->lat_axes) b.release();
     for (auto &b : c->lat_dk) b.release();
     for (auto &b : c->lat_recs) b.release();
+    for (auto &b : c->lat_order) b.release();
     c->slots.release();
     c->rbf_pw.release();
     c->rbf_status.release();
@@ -507,6 +509,15 @@ int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchP
             lat[l].recs = c->lat_recs[l].p;
         }
         KnnLaunch ll = kl;
+        const char *no_order = std::getenv("PTV_NO_LAT_ORDER");  // dev knob: 1 = XCD-contiguous order
+        if (!(no_order && no_order[0] == '1')) {
+            const long long nb = (long long)(((lat[l].n[0] + 3) / 4 + 3) / 4) * ((lat[l].n[1] + 3) / 4) *
+                                 ((lat[l].n[2] + 3) / 4);
+            PTV_TRY(c->lat_order[l].ensure((size_t)nb));
+            PTV_TRY(launch_block_order(lat[l + 1].dk, lat[l + 1].n, lat[l].n[0], lat[l].n[1], lat[l].n[2], kl.r0,
+                                       c->lat_order[l].p, s));
+            ll.order = c->lat_order[l].p;
+        }
         ll.kd_recs = lat[l].recs;
         ll.nx = lat[l].n[0];
         ll.ny = lat[l].n[1];

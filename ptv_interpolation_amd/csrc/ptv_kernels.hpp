@@ -60,7 +60,15 @@ struct KnnLaunch {
     float4 *kd_recs = nullptr;   // kModeKDist: also write each point's k-NN seed records here
     int lz0 = -1;                // plane of lattice point 0 (-1: z0); chunked launches keep the slab's
     uint32_t *slots = nullptr;   // kModeSlots: (z1 - z0, ny, nx, k) neighbour slots out
+    const int *order = nullptr;  // dispatch order of the launch's blocks (NULL: XCD-contiguous ranges)
 };
+
+// Longest-first dispatch order for a lattice-level k-NN launch over (nx, ny, nz) points: each
+// block (4 x 1 x 1 tiles of 4^3 points) is keyed by the largest coarser-level bound dk over the
+// coarser points around it (D / unit, 256 buckets), and `order` lists the blocks by descending
+// key, so the void tiles (long searches) start first instead of forming the launch's tail.
+int launch_block_order(const double *dk_coarse, const int nc[3], int nx, int ny, int nz, double unit, int *order,
+                       hipStream_t s);
 
 // Upper bound on the k-th neighbour distance of every point of a separable grid by
 // counting the particles of cells entirely inside balls around it (coarsest lattice).

@@ -79,6 +79,7 @@ struct KnnKernelArgs {
     uint32_t *slots;   // kModeSlots: neighbour slots out
     int seed_n;        // seed records used per lattice corner (<= k)
     int nblocks;       // workgroups of the launch (the grid may be 2-D, see launch_knn)
+    const int *order;  // block dispatch order (NULL: XCD-contiguous ranges)
 };
 
 // numpy pairwise sum of a[0..n) (n <= KMAX <= 128), from identity 0.0.
@@ -332,7 +333,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
     // particle records; each XCD has its own L2)
     const int lb = (int)(blockIdx.y * gridDim.x + blockIdx.x);  // linear dispatch order
     if (lb >= a.nblocks) return;                                  // 2-D grid padding (block-uniform)
-    const int b = xcd_block(lb, a.nblocks);
+    const int b = a.order != nullptr ? a.order[lb] : xcd_block(lb, a.nblocks);
     const int bx = b % a.ntxb;
     const int rr = b / a.ntxb;
     const int ty = rr % a.nty;
@@ -838,6 +839,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
     }
     stamp(t_setup);  // exactness checks / radius updates count as setup
 
+    // per-wave stamp record (ptv_debug_stamps), written by the first valid lane
+    auto write_stamps = [&]() {
+        if constexpr (STAMP) {
+            stamp(t_epi);
+            const long long gw = (long long)lb * 4 + wid;
+            if (dbg != nullptr && gw < dbg_cap && (threadIdx.x & 63) == (int)__builtin_ffsll((long long)__builtin_amdgcn_ballot_w64(true)) - 1) {
+                unsigned long long *r = dbg + gw * kStampFields;
+                r[0] = t_setup;
+                r[1] = t_seed;
+                r[2] = t_rows;
+                r[3] = t_copy;
+                r[4] = t_comp;
+                r[5] = t_epi;
+                r[6] = n_cand + ((unsigned long long)n_acc << 32);
+                r[7] = (n_round & 0xffffu) + ((unsigned long long)(n_pass & 0xffffu) << 16) + ((unsigned long long)n_surv << 32);
+            }
+        }
+    };
     if (!valid) return;
     const size_t vo = ((size_t)(iz - a.z0) * a.ny + iy) * a.nx + ix;
     if (a.mode == kModeKDist) {
@@ -859,6 +878,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
                 }
             }
         }
+        write_stamps();
         return;
     }
     if (a.mode == kModeSlots) {
@@ -977,21 +997,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
         for (int c = 0; c < 3; ++c) out[c] = nan_to_num(out[c]);
     }
     store_out(a.flags, U, V, W, vo, out[0], out[1], out[2]);
-    if constexpr (STAMP) {
-        stamp(t_epi);
-        const long long gw = (long long)lb * 4 + wid;
-        if (dbg != nullptr && gw < dbg_cap && (threadIdx.x & 63) == (int)__builtin_ffsll((long long)__builtin_amdgcn_ballot_w64(true)) - 1) {
-            unsigned long long *r = dbg + gw * kStampFields;
-            r[0] = t_setup;
-            r[1] = t_seed;
-            r[2] = t_rows;
-            r[3] = t_copy;
-            r[4] = t_comp;
-            r[5] = t_epi;
-            r[6] = n_cand + ((unsigned long long)n_acc << 32);
-            r[7] = (n_round & 0xffffu) + ((unsigned long long)(n_pass & 0xffffu) << 16) + ((unsigned long long)n_surv << 32);
-        }
-    }
+    write_stamps();
 }
 
 // ---------------------------------------------------------------------------
@@ -1132,6 +1138,58 @@ int launch_halo_need(const double *lax, const double *lay, const double *laz, in
     return PTV_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Longest-first block order of a lattice-level launch (one workgroup of 1024 threads: a
+// bucket histogram of the block keys in LDS, a scan, then placement by LDS atomics; the
+// order inside a bucket is arbitrary, which changes nothing but the dispatch order).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_block_order(const double *__restrict__ dkc, int cnx, int cny, int cnz,
+                                                      int ntxb, int nty, int nblocks, double inv_unit,
+                                                      int *__restrict__ order) {
+    __shared__ int cnt[256];
+    __shared__ int base[256];
+    auto bucket = [&](int b) -> int {
+        // block b: tiles (bx*4 .. bx*4+3, ty, tz) = points x [16 bx, 16 bx + 15], y [4 ty, 4 ty + 3],
+        // z [4 tz, 4 tz + 3]; coarser point j sits at point 4 j (kLatticeStep), so the block lies in
+        // the coarser cells spanned by x [4 bx, 4 bx + 4], y [ty, ty + 1], z [tz, tz + 1]
+        const int bx = b % ntxb, rr = b / ntxb, ty = rr % nty, tz = rr / nty;
+        double D = 0.0;
+        for (int z = tz; z <= tz + 1; ++z)
+            for (int y = ty; y <= ty + 1; ++y)
+                for (int x = 4 * bx; x <= 4 * bx + 4; ++x)
+                    D = fmax(D, dkc[((size_t)min(z, cnz - 1) * cny + min(y, cny - 1)) * cnx + min(x, cnx - 1)]);
+        const double q = D * inv_unit;
+        return 255 - (q < 255.0 ? (int)q : 255);  // descending bound -> ascending bucket
+    };
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) cnt[i] = 0;
+    __syncthreads();
+    for (int b = threadIdx.x; b < nblocks; b += blockDim.x) atomicAdd(&cnt[bucket(b)], 1);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int run = 0;
+        for (int i = 0; i < 256; ++i) {
+            base[i] = run;
+            run += cnt[i];
+        }
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < nblocks; b += blockDim.x) order[atomicAdd(&base[bucket(b)], 1)] = b;
+}
+
+int launch_block_order(const double *dk_coarse, const int nc[3], int nx, int ny, int nz, double unit, int *order,
+                       hipStream_t s) {
+    const int ntxb = ((nx + 3) / 4 + 3) / 4, nty = (ny + 3) / 4, ntz = (nz + 3) / 4;
+    const long long nblocks = (long long)ntxb * nty * ntz;
+    if (nblocks > 0x7fffffffLL || !(unit > 0.0)) {
+        set_error("lattice block order: bad launch shape");
+        return PTV_E_ARG;
+    }
+    hipLaunchKernelGGL(k_block_order, dim3(1), dim3(1024), 0, s, dk_coarse, nc[0], nc[1], nc[2], ntxb, nty,
+                       (int)nblocks, 8.0 / unit, order);
+    PTV_HIP(hipGetLastError());
+    return PTV_OK;
+}
+
 static const int kKmaxList[] = {4, 8, 12, 16, 24, 32, 40, 48, 56, 64};
 
 int kmax_for(int k) {
@@ -1145,7 +1203,10 @@ static void launch_t(dim3 grid, hipStream_t s, const KnnKernelArgs &ka, const Bi
                      const double *ay, const double *az, const double *qx, const double *qy, const double *qz,
                      const uint8_t *mask, double *U, double *V, double *W) {
     if constexpr (KMAX == 8) {
-        if (g_dbg != nullptr && ka.mode == kModeInterp) {
+        // stamps record the main launch, or the lattice-level launches under PTV_STAMP_LATTICE=1
+        const char *sl = std::getenv("PTV_STAMP_LATTICE");
+        const int stamp_mode = (sl && sl[0] == '1') ? kModeKDist : kModeInterp;
+        if (g_dbg != nullptr && ka.mode == stamp_mode) {
             hipLaunchKernelGGL((k_knn_interp<KMAX, true>), grid, dim3(256), 0, s, ka, b.prec, b.pval, b.cstart, ax, ay,
                                az, qx, qy, qz, mask, U, V, W, g_dbg, g_dbg_cap);
             return;
@@ -1188,6 +1249,7 @@ int launch_knn(const KnnLaunch &a, const Binned &b, const double *ax, const doub
     ka.kd_recs = a.kd_recs;
     ka.lz0 = a.lz0 < 0 ? a.z0 : a.lz0;
     ka.slots = a.slots;
+    ka.order = a.order;
     ka.seed_n = a.k;
     if (const char *e = std::getenv("PTV_SEED_N")) ka.seed_n = std::max(1, std::min(a.k, std::atoi(e)));  // dev knob
     if (a.mode == kModeSlots && (a.slots == nullptr || (a.z0 - ka.lz0) % 4 != 0)) {
