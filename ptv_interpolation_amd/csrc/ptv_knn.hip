@@ -50,6 +50,9 @@ namespace ptv {
 #ifndef PTV_KNN_WAVES
 #define PTV_KNN_WAVES 4  // waves per SIMD the k <= 8 kernels are register-capped for
 #endif
+#ifndef PTV_KNN_WAVES_BIG
+#define PTV_KNN_WAVES_BIG 1  // k > 8: no cap (the split modes reach 2 waves per SIMD up to KMAX = 32)
+#endif
 
 constexpr int kStampFields = 8;
 constexpr int kCap = 128;        // LDS candidate slots per wave (16 B fp32 + 32 B fp64 each)
@@ -299,8 +302,11 @@ __device__ __forceinline__ double axis_gap(int c, double o, double cs, double lo
     return fmax(fmax(c0 - hi, lo - c1), 0.0);
 }
 
-template <int KMAX, bool STAMP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ? PTV_KNN_WAVES : 1))) void k_knn_interp(KnnKernelArgs a, const double4 *__restrict__ prec,
+// MODE (kModeInterp / kModeKDist / kModeSlots) is a template parameter so that the search-only
+// modes carry no interpolation epilogue: one kernel for every mode put the KMAX = 32 lists at
+// 284 registers (one wave per SIMD); split, every KMAX <= 32 kernel runs two waves per SIMD.
+template <int KMAX, bool STAMP, int MODE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ? PTV_KNN_WAVES : PTV_KNN_WAVES_BIG))) void k_knn_interp(KnnKernelArgs a, const double4 *__restrict__ prec,
                                                     const double4 *__restrict__ pval,
                                                     const uint32_t *__restrict__ cstart,
                                                     const double *__restrict__ ax, const double *__restrict__ ay,
@@ -859,7 +865,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
     };
     if (!valid) return;
     const size_t vo = ((size_t)(iz - a.z0) * a.ny + iy) * a.nx + ix;
-    if (a.mode == kModeKDist) {
+    if constexpr (MODE == kModeKDist) {
         U[vo] = sqrt(bd[KMAX - 1]);
         if (a.kd_recs != nullptr) {
             // the k-NN records (list order) seed the next finer level's tiles: {p - this lattice
@@ -881,7 +887,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
         write_stamps();
         return;
     }
-    if (a.mode == kModeSlots) {
+    if constexpr (MODE == kModeSlots) {
         // the k neighbour slots (list order) for the local-RBF solve (ptv_rbf.hip)
         if (!active) return;
         uint32_t *o = a.slots + vo * (size_t)a.k;
@@ -1198,22 +1204,33 @@ int kmax_for(int k) {
     return 0;
 }
 
+template <int KMAX, int MODE>
+static void launch_m(dim3 grid, hipStream_t s, const KnnKernelArgs &ka, const Binned &b, const double *ax,
+                     const double *ay, const double *az, const double *qx, const double *qy, const double *qz,
+                     const uint8_t *mask, double *U, double *V, double *W) {
+    if constexpr (KMAX == 8 && MODE != kModeSlots) {
+        // stamps record the main launch, or the lattice-level launches under PTV_STAMP_LATTICE=1
+        const char *sl = std::getenv("PTV_STAMP_LATTICE");
+        const int stamp_mode = (sl && sl[0] == '1') ? kModeKDist : kModeInterp;
+        if (g_dbg != nullptr && MODE == stamp_mode) {
+            hipLaunchKernelGGL((k_knn_interp<KMAX, true, MODE>), grid, dim3(256), 0, s, ka, b.prec, b.pval, b.cstart,
+                               ax, ay, az, qx, qy, qz, mask, U, V, W, g_dbg, g_dbg_cap);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((k_knn_interp<KMAX, false, MODE>), grid, dim3(256), 0, s, ka, b.prec, b.pval, b.cstart, ax, ay,
+                       az, qx, qy, qz, mask, U, V, W, (unsigned long long *)nullptr, 0LL);
+}
+
 template <int KMAX>
 static void launch_t(dim3 grid, hipStream_t s, const KnnKernelArgs &ka, const Binned &b, const double *ax,
                      const double *ay, const double *az, const double *qx, const double *qy, const double *qz,
                      const uint8_t *mask, double *U, double *V, double *W) {
-    if constexpr (KMAX == 8) {
-        // stamps record the main launch, or the lattice-level launches under PTV_STAMP_LATTICE=1
-        const char *sl = std::getenv("PTV_STAMP_LATTICE");
-        const int stamp_mode = (sl && sl[0] == '1') ? kModeKDist : kModeInterp;
-        if (g_dbg != nullptr && ka.mode == stamp_mode) {
-            hipLaunchKernelGGL((k_knn_interp<KMAX, true>), grid, dim3(256), 0, s, ka, b.prec, b.pval, b.cstart, ax, ay,
-                               az, qx, qy, qz, mask, U, V, W, g_dbg, g_dbg_cap);
-            return;
-        }
+    switch (ka.mode) {
+        case kModeKDist: launch_m<KMAX, kModeKDist>(grid, s, ka, b, ax, ay, az, qx, qy, qz, mask, U, V, W); break;
+        case kModeSlots: launch_m<KMAX, kModeSlots>(grid, s, ka, b, ax, ay, az, qx, qy, qz, mask, U, V, W); break;
+        default: launch_m<KMAX, kModeInterp>(grid, s, ka, b, ax, ay, az, qx, qy, qz, mask, U, V, W);
     }
-    hipLaunchKernelGGL((k_knn_interp<KMAX, false>), grid, dim3(256), 0, s, ka, b.prec, b.pval, b.cstart, ax, ay, az,
-                       qx, qy, qz, mask, U, V, W, (unsigned long long *)nullptr, 0LL);
 }
 
 int launch_knn(const KnnLaunch &a, const Binned &b, const double *ax, const double *ay, const double *az,
