@@ -54,6 +54,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Mvoxels/s interpolated + achieved HBM GB/s, 512³ grid / 5M particles IDW"
 METRIC_C2 = "Mvoxels/s interpolated + achieved HBM GB/s, 256³ grid / 1M particles IDW"
+METRIC_C2R = "Mvoxels/s interpolated + achieved HBM GB/s, 256³ grid / 1M particles IDW radius-search"
 METRIC_RBF = "Mvoxels/s interpolated + achieved FP64 TFLOP/s, 512³ grid / 5M particles local RBF"
 METRIC_C4 = "Mvoxels/s interpolated + achieved HBM GB/s, 1024³ grid / 10M particles masked IDW (z-slab partition)"
 METRIC_C5 = ("Mvoxels/s interpolated + achieved HBM GB/s, 2048³ grid / 50M particles fp32 IDW + divergence "
@@ -70,6 +71,9 @@ KMAX_LIST = (4, 8, 12, 16, 24, 32, 40, 48, 56, 64)  # k_knn_interp instantiation
 CONFIGS = {
     "headline": dict(grid=512, particles=5_000_000, method="idw", k=8, scaling="weak", metric=METRIC),
     "c2": dict(grid=256, particles=1_000_000, method="idw", k=8, scaling="strong", metric=METRIC_C2),
+    # BASELINE config 2 as named ("IDW radius-search"): an extension, the reference has no radius
+    # search (parity unpinned; tests/test_gpu_radius.py); r = 3 voxels ~ 6.8 particles per ball
+    "c2r": dict(grid=256, particles=1_000_000, method="idw", k=8, radius=3.0, scaling="strong", metric=METRIC_C2R),
     "c3": dict(grid=512, particles=5_000_000, method="rbf", k=32, rbf_kernel="gaussian", epsilon=0.3, degree=-1,
                scaling="strong", metric=METRIC_RBF),
     "c4": dict(grid=1024, particles=10_000_000, method="idw", k=8, mask=True, scaling="strong", metric=METRIC_C4),
@@ -110,6 +114,8 @@ def parse():
     ap.add_argument("--particles", type=int, default=None)
     ap.add_argument("--k", type=int, default=None)
     ap.add_argument("--power", type=float, default=2.0)
+    ap.add_argument("--radius", type=float, default=None,
+                    help="idw: fixed-radius search (PTV_METHOD_IDW_RADIUS, an extension) instead of k-NN")
     ap.add_argument("--method", default=None, choices=["idw", "sibson", "nearest", "rbf", "div", "filter", "mask"])
     ap.add_argument("--div-dtype", default="f64", choices=["f64", "f32"],
                     help="--method div: field dtype (f32 = the C5 fp32 field, Python-float spacings)")
@@ -136,7 +142,7 @@ def parse():
     defaults = dict(grid=cfg["grid"], particles=cfg["particles"], method=cfg["method"], k=cfg["k"],
                     rbf_kernel=cfg.get("rbf_kernel", "thin_plate_spline"), epsilon=cfg.get("epsilon"),
                     degree=cfg.get("degree"), out_dtype=cfg.get("out_dtype", "f64"), mask=cfg.get("mask", False),
-                    div=cfg.get("div", False))
+                    div=cfg.get("div", False), radius=cfg.get("radius", 0.0))
     for key, v in defaults.items():
         if getattr(a, key) is None:
             setattr(a, key, v)
@@ -229,6 +235,42 @@ def cpu_baseline(args, P, Q, ax, az, z0_grid):
                      f"{planes} central z-planes ({nvox} voxels) of the same {args.grid}^3/{args.particles} workload "
                      f"(mask not applied); scipy KDTree + numpy (oracle/cpu_ref.py), {workers} processes, each "
                      f"building its own tree (interpolator.py:173-182 pattern)", dt)
+
+
+_BALL = {}
+
+
+def ball_population(P, ax, radius, nsample=20000):
+    """Mean number of particles within `radius` of a grid voxel (seeded voxel sample)."""
+    key = (id(P), radius)
+    if key not in _BALL:
+        from scipy.spatial import KDTree
+
+        G = len(ax)
+        rng = np.random.default_rng(1)
+        iz, iy, ix = np.unravel_index(rng.integers(0, G ** 3, nsample), (G, G, G))
+        q = np.stack([ax[ix], ax[iy], ax[iz]], 1)
+        _BALL[key] = float(np.mean(KDTree(P).query_ball_point(q, radius, return_length=True)))
+    return _BALL[key]
+
+
+def cpu_baseline_radius(args, P, Q, ax, radius):
+    """The fixed-radius IDW restatement (oracle/cpu_ref.idw_radius_points: KDTree
+    query_ball_point + numpy per voxel) on a bounded random voxel sample, one process."""
+    from oracle import cpu_ref
+
+    G = len(ax)
+    nvox = 100_000
+    rng = np.random.default_rng(0)
+    iz, iy, ix = np.unravel_index(rng.integers(0, G ** 3, nvox), (G, G, G))
+    q = np.stack([ax[ix], ax[iy], ax[iz]], -1)
+    t = time.perf_counter()
+    cpu_ref.idw_radius_points(P, Q, q, radius, power=args.power)
+    dt = time.perf_counter() - t
+    return _cpu_line(round(nvox / dt / 1e6, 4), "Mvoxels/s", 1,
+                     f"{nvox} random voxels of the same {G}^3/{args.particles} workload, radius {radius}; scipy "
+                     f"KDTree query_ball_point + numpy (oracle/cpu_ref.idw_radius_points), 1 process "
+                     f"(no reference counterpart: kind 'port')", dt)
 
 
 def _rbf_cpu_worker(a):
@@ -370,7 +412,10 @@ def main_interp(args):
     ctx = _lib.Context(local)
     stream = torch.cuda.current_stream(dev).cuda_stream
     method = {"idw": _lib.METHOD_IDW, "sibson": _lib.METHOD_SIBSON, "nearest": _lib.METHOD_NEAREST}.get(args.method)
-    cull = world > 1 and not rbf
+    radius = args.radius if (args.radius and args.method == "idw") else 0.0
+    if radius:
+        method = _lib.METHOD_IDW_RADIUS
+    cull = world > 1 and not rbf and not radius
     halo = zslab.HaloState(args.halo if args.halo is not None else
                            zslab.halo_guess(n, (G, G, nz), k))
     ptrs = [c.data_ptr() for c in cols]
@@ -390,7 +435,7 @@ def main_interp(args):
         def call(h):
             return ctx.interp_knn_dev(n, ptrs, G, G, nz, axes_ptrs=aptrs, out_ptrs=optrs, method=method, k=k,
                                       power=args.power, stream=stream, mask_ptr=mptr, r0_scale=args.r0_scale,
-                                      flags=flags, z_range=(za, zb), slab_halo=h)
+                                      flags=flags, z_range=(za, zb), slab_halo=h, radius=radius)
 
         zslab.interp_slab(call, halo) if cull else call(0.0)
         if args.div:
@@ -452,6 +497,8 @@ def main_interp(args):
             grid, _ = ip.create_grid(((0, G), (0, G), (0, G)), G, dense=False)
             kw = {"idw": dict(idw_neighbors=k, idw_power=args.power), "sibson": dict(sibson_neighbors=k),
                   "nearest": {}}[args.method]
+            if radius:
+                kw["idw_radius"] = radius
             walls = []
             os.environ["PTV_DEVICE"] = str(local)  # this rank's GPU only (launcher.devices())
             for _ in range(2):  # first call allocates the context's host-path buffers
@@ -479,7 +526,10 @@ def main_interp(args):
                 "knn_slots_ms": round(avg["ms_knn"], 3)}
     else:
         Vk = (zb - za) * G * G  # voxels the k-NN launch computes (slab + redundant halo planes)
-        if args.mask:  # solid voxels are skipped: fluid V in the gather term, + the mask byte
+        if radius:  # gather model with the measured mean ball population in place of k
+            k_eff = ball_population(P, ax_h, radius) if P is not None else 0.0
+            alg = int(round(Vk * (6 * k_eff * 8 + 3 * s_out)))
+        elif args.mask:  # solid voxels are skipped: fluid V in the gather term, + the mask byte
             alg = int(round(Vk * fluid_frac)) * 6 * k * 8 + Vk * (3 * s_out + 1)
         else:
             alg = Vk * (6 * k * 8 + 3 * s_out)
@@ -490,7 +540,8 @@ def main_interp(args):
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBPS, 4),
                 "traffic": traffic_from_profiles() if headline_shape else None,
-                "kernel": f"k_knn_interp<{kmax_for(k)}>", "alg_bytes_per_launch": alg,
+                "kernel": "k_knn_interp<4, radius>" if radius else f"k_knn_interp<{kmax_for(k)}>",
+                "alg_bytes_per_launch": alg,
                 "kernel_ms": round(avg["ms_knn"], 3),
                 "frac_step": round(alg_step / (t_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                 "step_device_ms": round(t_step, 3)}
@@ -504,7 +555,9 @@ def main_interp(args):
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and P is not None:
         try:
-            cpu = cpu_baseline_rbf(args, P, Q, ax_h) if rbf else cpu_baseline(args, P, Q, ax_h, az_h, 0)
+            cpu = (cpu_baseline_rbf(args, P, Q, ax_h) if rbf else
+                   cpu_baseline_radius(args, P, Q, ax_h, radius) if radius else
+                   cpu_baseline(args, P, Q, ax_h, az_h, 0))
         except Exception as e:  # the baseline must never take the GPU line down
             cpu = {"value": None, "error": repr(e)[:200]}
 
@@ -519,7 +572,9 @@ def main_interp(args):
         if rbf:
             wl += f"; local RBF {kern} k={k} eps={eps} degree={deg} (system {m_sys}) fp64"
         else:
-            wl += (f"; {args.method.upper()} k={k} p={args.power} fp64" + (" (float32 U, V, W)" if out_f32 else "") +
+            wl += ((f"; IDW radius={radius} (mean ball {ball_population(P, ax_h, radius):.2f} particles) p={args.power} fp64"
+                    if radius else f"; {args.method.upper()} k={k} p={args.power} fp64") +
+                   (" (float32 U, V, W)" if out_f32 else "") +
                    (f" + sphere-pack fluid mask ({fluid_frac:.1%} fluid, solid skipped)" if args.mask else "") +
                    (" + consistent divergence (one-plane halo interpolated)" if args.div else ""))
         line = {

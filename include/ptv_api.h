@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define PTV_API_VERSION 5
+#define PTV_API_VERSION 6
 
 /* error codes */
 #define PTV_OK 0
@@ -39,6 +39,11 @@ extern "C" {
 #define PTV_METHOD_IDW 0
 #define PTV_METHOD_SIBSON 1
 #define PTV_METHOD_NEAREST 2
+/* Extension (no reference counterpart; parity unpinned): IDW over every particle
+ * within ptv_knn_params.radius of the voxel (scipy query_ball_point's d2 <= r*r test), weights
+ * 1/(d**power + eps) as interpolator.py:142-147, out = sum w u / sum w; an empty ball gives NaN.
+ * k is ignored.  BASELINE config 2 ("IDW radius-search"). */
+#define PTV_METHOD_IDW_RADIUS 3
 
 /* local RBF kernels (scipy RBFInterpolator names, _rbfinterp.py:19-28) */
 #define PTV_RBF_LINEAR 0
@@ -113,6 +118,7 @@ typedef struct {
      * interpolation when slab_halo is smaller (retry with halo_required, or 0 = no cull).
      * <= 0: every particle is binned (no check needed).  k-NN interpolation entry points only. */
     double slab_halo;
+    double radius;         /* PTV_METHOD_IDW_RADIUS: the search radius (> 0) */
 } ptv_knn_params;
 
 /*

@@ -195,6 +195,29 @@ def interp_points(points, values, queries, method="idw", k=8, power=2.0, knn="kd
         return gather_sum(w, values, idx)
 
 
+def idw_radius_points(points, values, queries, radius, power=2.0, eps=EPS):
+    """Fixed-radius IDW -- an EXTENSION with no reference counterpart (the reference only has
+    the k-NN ``tree.query``, interpolator.py:139), so parity is unpinned: this restatement
+    defines it for the GPU's PTV_METHOD_IDW_RADIUS.  Per query: every particle with
+    ``((dx*dx + dy*dy) + dz*dz) <= r*r`` (scipy ``KDTree.query_ball_point``'s test), weights
+    ``1/(d**p + eps)`` with numpy's scalar power (as interpolator.py:142-147), and
+    ``sum(w * v) / sum(w)``; an empty ball gives NaN.  Returns (M, 3) float64."""
+    from scipy.spatial import KDTree
+
+    points = np.asarray(points, dtype=np.float64)
+    values = np.asarray(values, dtype=np.float64)
+    q = np.asarray(queries, dtype=np.float64).reshape(-1, 3)
+    out = np.full((len(q), 3), np.nan)
+    for i, idx in enumerate(KDTree(points).query_ball_point(q, radius, return_sorted=True)):
+        if not idx:
+            continue
+        dd = q[i] - points[idx]
+        d = np.sqrt((dd[:, 0] * dd[:, 0] + dd[:, 1] * dd[:, 1]) + dd[:, 2] * dd[:, 2])
+        w = 1.0 / (numpy_power(d, power) + eps)
+        out[i] = (w[:, None] * values[idx]).sum(axis=0) / w.sum()
+    return out
+
+
 def grid_queries(ax, ay, az, z0=0, z1=None):
     """Voxel coordinates of the C-order (nz, ny, nx) grid, x fastest (interpolator.py:59,135)."""
     z1 = len(az) if z1 is None else z1

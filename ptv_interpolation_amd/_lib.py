@@ -26,6 +26,7 @@ PTV_E_SINGULAR = -6
 METHOD_IDW = 0
 METHOD_SIBSON = 1
 METHOD_NEAREST = 2
+METHOD_IDW_RADIUS = 3  # extension: IDW over every particle within a radius (parity unpinned)
 
 FLAG_NAN_TO_NUM = 1
 
@@ -58,7 +59,8 @@ class Grid(C.Structure):
 class KnnParams(C.Structure):
     _fields_ = [("method", C.c_int), ("k", C.c_int), ("power", C.c_double), ("eps", C.c_double),
                 ("fluid_mask", C.POINTER(C.c_uint8)), ("flags", C.c_uint32), ("cell_occupancy", C.c_double),
-                ("r0_scale", C.c_double), ("lattice_bounds", C.c_int), ("slab_halo", C.c_double)]
+                ("r0_scale", C.c_double), ("lattice_bounds", C.c_int), ("slab_halo", C.c_double),
+                ("radius", C.c_double)]
 
 
 class RbfParams(C.Structure):
@@ -405,7 +407,7 @@ class Context:
     # -- host buffers ------------------------------------------------------
     def interp_knn(self, points, values, axes=None, grid_points=None, shape=None, method=METHOD_IDW, k=8,
                    power=2.0, eps=1e-10, fluid_mask=None, flags=0, z_range=None, cell_occupancy=0.0,
-                   r0_scale=0.0, lattice_bounds=0, slab_halo=0.0, out=None):
+                   r0_scale=0.0, lattice_bounds=0, slab_halo=0.0, out=None, radius=0.0):
         """Host-array k-NN interpolation. Returns (U, V, W) float64 (nz', ny, nx).
 
         ``out``: optional three C-contiguous (nz', ny, nx) arrays of the output dtype (e.g.
@@ -428,7 +430,7 @@ class Context:
                 res = self.interp_knn(points, values, grid_points=gp, shape=tshape, method=method, k=k,
                                       power=power, eps=eps, fluid_mask=fm, flags=flags,
                                       cell_occupancy=cell_occupancy, r0_scale=r0_scale,
-                                      lattice_bounds=lattice_bounds)
+                                      lattice_bounds=lattice_bounds, radius=radius)
                 return tuple(unpad(a) for a in res)
             nz, ny, nx = shape
             keep += gp
@@ -441,7 +443,8 @@ class Context:
             keep.append(mk)
         prm = KnnParams(method, int(k), float(power), float(eps),
                         mk.ctypes.data_as(C.POINTER(C.c_uint8)) if mk is not None else None, flags,
-                        float(cell_occupancy), float(r0_scale), int(lattice_bounds), float(slab_halo))
+                        float(cell_occupancy), float(r0_scale), int(lattice_bounds), float(slab_halo),
+                        float(radius))
         odt = np.float32 if flags & FLAG_OUT_F32 else np.float64
         out = _outputs(out, (z1 - z0, ny, nx), odt)
         st = Stats()
@@ -525,7 +528,7 @@ class Context:
     # -- device buffers (integer device pointers, e.g. torch tensor data_ptr()) --
     def interp_knn_dev(self, n, pptrs, nx, ny, nz, axes_ptrs=None, point_ptrs=None, out_ptrs=None,
                        method=METHOD_IDW, k=8, power=2.0, eps=1e-10, mask_ptr=0, flags=0, z_range=None,
-                       stream=0, cell_occupancy=0.0, r0_scale=0.0, lattice_bounds=0, slab_halo=0.0):
+                       stream=0, cell_occupancy=0.0, r0_scale=0.0, lattice_bounds=0, slab_halo=0.0, radius=0.0):
         """Device-pointer k-NN interpolation (inputs resident in HBM), enqueued on `stream`;
         returns the call's stats.  ``slab_halo`` > 0: see ptv_knn_params.slab_halo (raises
         InexactError carrying ``halo_required`` when the halo is too small)."""
@@ -538,7 +541,8 @@ class Context:
         G.z_begin, G.z_end = z0, z1
         prm = KnnParams(method, int(k), float(power), float(eps),
                         C.cast(C.c_void_p(mask_ptr), C.POINTER(C.c_uint8)) if mask_ptr else None, flags,
-                        float(cell_occupancy), float(r0_scale), int(lattice_bounds), float(slab_halo))
+                        float(cell_occupancy), float(r0_scale), int(lattice_bounds), float(slab_halo),
+                        float(radius))
         st = Stats()
         rc = lib().ptv_interp_knn_dev(self.h, C.byref(P), C.byref(G), C.byref(prm),
                                       *[dev_dp(p) for p in out_ptrs], C.c_void_p(stream or 0), C.byref(st))

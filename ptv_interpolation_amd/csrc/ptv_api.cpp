@@ -287,9 +287,17 @@ int validate(const ptv_particles *p, const ptv_grid *g, const void *prm) {
 }
 
 int validate_knn(const ptv_particles *p, const ptv_knn_params *prm) {
-    if (prm->method != PTV_METHOD_IDW && prm->method != PTV_METHOD_SIBSON && prm->method != PTV_METHOD_NEAREST) {
+    if (prm->method != PTV_METHOD_IDW && prm->method != PTV_METHOD_SIBSON && prm->method != PTV_METHOD_NEAREST &&
+        prm->method != PTV_METHOD_IDW_RADIUS) {
         set_error("unknown method " + std::to_string(prm->method));
         return PTV_E_ARG;
+    }
+    if (prm->method == PTV_METHOD_IDW_RADIUS) {
+        if (!(prm->radius > 0.0 && std::isfinite(prm->radius))) {
+            set_error("PTV_METHOD_IDW_RADIUS needs a positive finite radius");
+            return PTV_E_ARG;
+        }
+        return PTV_OK;  // k is not used
     }
     if (prm->k < 1) {
         set_error("k must be >= 1");
@@ -579,14 +587,20 @@ SearchParams knn_search(const ptv_knn_params *prm) {
 int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn_params *prm, const double *ax,
             const double *ay, const double *az, const double *qx, const double *qy, const double *qz,
             const uint8_t *mask, double *U, double *V, double *W, hipStream_t s, ptv_stats *st) {
-    const SearchParams sp = knn_search(prm);
+    SearchParams sp = knn_search(prm);
+    const bool radius = prm->method == PTV_METHOD_IDW_RADIUS;
+    if (radius) {
+        // fixed-radius IDW: one pass over the radius ball, no k-th distance bounds or seeds
+        sp.k = 1;
+        sp.lattice_bounds = -1;
+    }
     KnnLaunch kl;
     Binned b{};
     // slab cull (ptv_knn_params.slab_halo): bin only the particles near this z-slab
     ptv_particles pe = *p;
     bool culled = false;
     c->cull_timed = false;
-    if (prm->slab_halo > 0.0 && ax != nullptr && lattice_built(g, prm->lattice_bounds)) {
+    if (!radius && prm->slab_halo > 0.0 && ax != nullptr && lattice_built(g, prm->lattice_bounds)) {
         const int64_t n = p->n;
         const size_t nb = cull_blocks(n);
         for (auto &d : c->cull) PTV_TRY(d.ensure(n));
@@ -636,6 +650,10 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
         PTV_HIP(hipEventRecord(c->ev_main0, s));
     }
     c->rbf_chunks = 0;
+    if (radius) {
+        kl.mode = kModeRadius;
+        kl.radius = prm->radius;
+    }
     PTV_TRY(launch_knn(kl, b, ax, ay, az, qx, qy, qz, mask, U, V, W, s));
     PTV_HIP(hipEventRecord(c->ev_knn1, s));
     c->timed_pending = true;

@@ -44,6 +44,7 @@ struct CoarseBound {
 constexpr int kModeInterp = 0;  // write U, V, W
 constexpr int kModeKDist = 1;   // write the exact k-th neighbour distance into U
 constexpr int kModeSlots = 2;   // write each voxel's k neighbour slots (sorted-record indices)
+constexpr int kModeRadius = 3;  // IDW over every particle within a fixed radius (PTV_METHOD_IDW_RADIUS)
 
 struct KnnLaunch {
     CellGrid cg;
@@ -60,6 +61,7 @@ struct KnnLaunch {
     float4 *kd_recs = nullptr;   // kModeKDist: also write each point's k-NN seed records here
     int lz0 = -1;                // plane of lattice point 0 (-1: z0); chunked launches keep the slab's
     uint32_t *slots = nullptr;   // kModeSlots: (z1 - z0, ny, nx, k) neighbour slots out
+    double radius = 0.0;         // kModeRadius: the search radius
     const int *order = nullptr;  // dispatch order of the launch's blocks (NULL: XCD-contiguous ranges)
 };
 

@@ -82,6 +82,7 @@ struct KnnKernelArgs {
     uint32_t *slots;   // kModeSlots: neighbour slots out
     int seed_n;        // seed records used per lattice corner (<= k)
     int nblocks;       // workgroups of the launch (the grid may be 2-D, see launch_knn)
+    double radius;     // kModeRadius: every particle with d2 <= radius^2 (query_ball_point's test)
     const int *order;  // block dispatch order (NULL: XCD-contiguous ranges)
 };
 
@@ -328,6 +329,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
     __shared__ __attribute__((aligned(16))) float lds_cfx[4][kCap], lds_cfy[4][kCap], lds_cfz[4][kCap];
     __shared__ uint2 lds_runs[4][kRunEntries];
     __shared__ int lds_owner[4][64];
+    // kModeRadius: the value records of the buffered candidates (the weights are summed in the flush)
+    __shared__ double4 lds_val[4][MODE == kModeRadius ? kCap : 1];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     double4 *buf = lds_cand[wid];
@@ -406,6 +409,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
     }
     // candidates at or beyond the bound can never be among the k nearest
     double ub2 = !active ? -1.0 : (ub < INFINITY ? ub * ub : INFINITY);
+    // radius mode: every candidate with d2 <= R^2 counts (the list stays unused)
+    const double rad2 = a.radius * a.radius;
+    double rs = 0.0, rsu = 0.0, rsv = 0.0, rsw = 0.0;  // sum w, sum w*u, sum w*v, sum w*w
+    if constexpr (MODE == kModeRadius) ub2 = !active ? -1.0 : rad2 * (1.0 + 2.220446049250313e-16) + 1e-300;
 
     // sorted list: KMAX-k front sentinels (-1) so bd[KMAX-1] is the k-th best.
     // Inactive lanes (padding / solid voxels) hold -1 everywhere: they never accept a
@@ -534,6 +541,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
         // a tight lattice bound (fine level) is used directly in one pass; a loose one
         // (coarse level) is preceded by a pass at the density radius r0.
         if (R_ub < INFINITY) R = (seeded || R_ub <= 2.0 * a.r0) ? R_ub : a.r0;
+        if constexpr (MODE == kModeRadius) R = a.radius;  // one pass
         // ---- sub-balls: the tile's 8 sub-boxes of 2x2x2 voxels (lanes differing in bits 0, 2, 4),
         //      each with centre c_s and radius max_v sqrt(thr_v) + |v - c_s|: a candidate outside
         //      every sub-ball can never enter any list (thresholds only shrink), so the copy drops it.
@@ -614,9 +622,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
                     const double4 c = gbuf[lz];
                     const double dx = qx - c.x, dy = qy - c.y, dz = qz - c.z;
                     const double e2 = (dx * dx + dy * dy) + dz * dz;
-                    const double d2 = (has && e2 < thr) ? e2 : INFINITY;
-                    insert<KMAX>(bd, bp, d2, (int)__double_as_longlong(c.w));  // no-op where d2 = inf
-                    thr = dmin(bd[KMAX - 1], ub2);
+                    if constexpr (MODE == kModeRadius) {
+                        // IDW term of a particle inside the ball (cKDTree's d2 <= r*r test)
+                        if (has && active && e2 <= rad2) {
+                            const double4 val = lds_val[wid][gbuf - buf + lz];
+                            const double w = 1.0 / (np_pow(sqrt_cr(e2), a.power) + a.eps);
+                            rs += w;
+                            rsu += w * val.x;
+                            rsv += w * val.y;
+                            rsw += w * val.z;
+                        }
+                    } else {
+                        const double d2 = (has && e2 < thr) ? e2 : INFINITY;
+                        insert<KMAX>(bd, bp, d2, (int)__double_as_longlong(c.w));  // no-op where d2 = inf
+                        thr = dmin(bd[KMAX - 1], ub2);
+                    }
                 }
                 thrf = f32_bound(thr, cpass);
             }
@@ -807,6 +827,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
                         const int pos = nbuf + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(km >> 32),
                                                                               __builtin_amdgcn_mbcnt_lo((unsigned)km, 0u));
                         buf[pos] = make_double4(p4.x, p4.y, p4.z, __longlong_as_double((long long)slot));
+                        if constexpr (MODE == kModeRadius) lds_val[wid][pos] = pval[slot];
                         fbx[pos] = ex;
                         fby[pos] = ey;
                         fbz[pos] = ez;
@@ -820,7 +841,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
             flush();
             // ---- exactness: lanes with k-th distance <= R are final ----
             const double worst = uniform(wave_max(bd[KMAX - 1]));  // inactive lanes hold -1
-            if (worst <= R * R || R >= a.rall) break;
+            if (MODE == kModeRadius || worst <= R * R || R >= a.rall) break;
             Rp = R;
             py0 = ry0;
             py1 = ry1;
@@ -898,6 +919,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
     }
     if (!active) {
         store_out(a.flags, U, V, W, vo, 0.0, 0.0, 0.0);
+        return;
+    }
+    if constexpr (MODE == kModeRadius) {
+        // sum_j w_j u_j / sum_j w_j (an empty ball gives 0 / 0 = NaN, "no data")
+        double o[3] = {rsu / rs, rsv / rs, rsw / rs};
+        if (a.flags & PTV_FLAG_NAN_TO_NUM) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) o[c] = nan_to_num(o[c]);
+        }
+        store_out(a.flags, U, V, W, vo, o[0], o[1], o[2]);
         return;
     }
 
@@ -1229,6 +1260,9 @@ static void launch_t(dim3 grid, hipStream_t s, const KnnKernelArgs &ka, const Bi
     switch (ka.mode) {
         case kModeKDist: launch_m<KMAX, kModeKDist>(grid, s, ka, b, ax, ay, az, qx, qy, qz, mask, U, V, W); break;
         case kModeSlots: launch_m<KMAX, kModeSlots>(grid, s, ka, b, ax, ay, az, qx, qy, qz, mask, U, V, W); break;
+        case kModeRadius:
+            if constexpr (KMAX == 4) launch_m<KMAX, kModeRadius>(grid, s, ka, b, ax, ay, az, qx, qy, qz, mask, U, V, W);
+            break;
         default: launch_m<KMAX, kModeInterp>(grid, s, ka, b, ax, ay, az, qx, qy, qz, mask, U, V, W);
     }
 }
@@ -1236,7 +1270,7 @@ static void launch_t(dim3 grid, hipStream_t s, const KnnKernelArgs &ka, const Bi
 int launch_knn(const KnnLaunch &a, const Binned &b, const double *ax, const double *ay, const double *az,
                const double *qx, const double *qy, const double *qz, const uint8_t *mask, double *U, double *V,
                double *W, hipStream_t s) {
-    const int km = kmax_for(a.k);
+    const int km = a.mode == kModeRadius ? 4 : kmax_for(a.k);
     if (km == 0) {
         set_error("k=" + std::to_string(a.k) + " exceeds the GPU k-NN list limit (64)");
         return PTV_E_UNSUPPORTED;
@@ -1266,6 +1300,11 @@ int launch_knn(const KnnLaunch &a, const Binned &b, const double *ax, const doub
     ka.kd_recs = a.kd_recs;
     ka.lz0 = a.lz0 < 0 ? a.z0 : a.lz0;
     ka.slots = a.slots;
+    ka.radius = a.radius;
+    if (a.mode == kModeRadius && !(a.radius > 0.0 && a.radius < INFINITY)) {
+        set_error("radius search needs a positive finite radius");
+        return PTV_E_ARG;
+    }
     ka.order = a.order;
     ka.seed_n = a.k;
     if (const char *e = std::getenv("PTV_SEED_N")) ka.seed_n = std::max(1, std::min(a.k, std::atoi(e)));  // dev knob

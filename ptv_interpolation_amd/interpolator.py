@@ -196,42 +196,61 @@ def _gpu_device():
     return launcher.devices()[0]
 
 
-def _knn_field(points, values, grid_tuple, method, k, power):
-    """GPU k-NN IDW/Sibson over the caller's grid; returns (U, V, W) with X's shape."""
+def _knn_field(points, values, grid_tuple, method, k, power, radius=0.0):
+    """GPU k-NN IDW/Sibson (or fixed-radius IDW) over the caller's grid; returns (U, V, W)
+    with X's shape."""
     X, Y, Z = grid_tuple
     shape = np.shape(X)
     n = points.shape[0]
-    if k < 1:
-        raise ValueError(f"k must be a positive integer, got {k}")
-    if n == 0:
-        raise ValueError("no particles to interpolate from")
-    if k == 1 and method != "nearest":
-        # the reference's KDTree.query(k=1) squeezes to (V,), then .sum(axis=1) fails
-        raise np.exceptions.AxisError("axis 1 is out of bounds for array of dimension 1")
-    if k > n:
-        # KDTree pads missing neighbours with index n; values[indices] then fails
-        raise IndexError(f"index {n} is out of bounds for axis 0 with size {n}")
-    m = {"idw": _lib.METHOD_IDW, "sibson": _lib.METHOD_SIBSON, "nearest": _lib.METHOD_NEAREST}[method]
+    if method == "idw_radius":
+        # extension (no reference counterpart): k is not used
+        if not (np.isfinite(radius) and radius > 0):
+            raise ValueError(f"idw_radius must be a positive finite number, got {radius}")
+        if n == 0:
+            raise ValueError("no particles to interpolate from")
+        k = 1
+    else:
+        if k < 1:
+            raise ValueError(f"k must be a positive integer, got {k}")
+        if n == 0:
+            raise ValueError("no particles to interpolate from")
+        if k == 1 and method != "nearest":
+            # the reference's KDTree.query(k=1) squeezes to (V,), then .sum(axis=1) fails
+            raise np.exceptions.AxisError("axis 1 is out of bounds for array of dimension 1")
+        if k > n:
+            # KDTree pads missing neighbours with index n; values[indices] then fails
+            raise IndexError(f"index {n} is out of bounds for axis 0 with size {n}")
+    m = {"idw": _lib.METHOD_IDW, "sibson": _lib.METHOD_SIBSON, "nearest": _lib.METHOD_NEAREST,
+         "idw_radius": _lib.METHOD_IDW_RADIUS}[method]
     axes = separable_axes(X, Y, Z)
     if axes is not None:
         # z-slab per device (launcher.py); bit-identical to one whole-grid call
         full = [np.empty((len(axes[2]), len(axes[1]), len(axes[0]))) for _ in range(3)]
         U, V, W = launcher.run_slabs(len(axes[2]), lambda ctx, z0, z1, views: ctx.interp_knn(
-            points, values, axes=axes, method=m, k=k, power=power, eps=_EPS, z_range=(z0, z1), out=views), full)
+            points, values, axes=axes, method=m, k=k, power=power, eps=_EPS, z_range=(z0, z1), out=views,
+            radius=radius), full)
     else:
         ctx = _lib.Context.get(launcher.devices()[0])
         size = int(np.prod(shape))
         g = [np.ascontiguousarray(np.asarray(A, dtype=np.float64)).reshape(-1) for A in (X, Y, Z)]
         sh = tuple(shape) if len(shape) == 3 else (1, 1, size)
-        U, V, W = ctx.interp_knn(points, values, grid_points=g, shape=sh, method=m, k=k, power=power, eps=_EPS)
+        U, V, W = ctx.interp_knn(points, values, grid_points=g, shape=sh, method=m, k=k, power=power, eps=_EPS,
+                                 radius=radius)
     return U.reshape(shape), V.reshape(shape), W.reshape(shape)
 
 
 def interpolate_field(df, grid_tuple, method="linear", rbf_neighbors=20, rbf_kernel="thin_plate_spline",
-                      smoothing=0.0, n_jobs=1, idw_power=2.0, idw_neighbors=50, sibson_neighbors=30):
+                      smoothing=0.0, n_jobs=1, idw_power=2.0, idw_neighbors=50, sibson_neighbors=30,
+                      idw_radius=None):
     """Interpolate PTV particles onto the grid (interpolator.py:65-203 signature and semantics).
 
     Returns ``(U, V, W)`` float64 arrays of the grid's shape.
+
+    ``idw_radius`` (extension, not in the reference): with ``method='idw'``, weight every particle
+    within this distance of the voxel (scipy ``query_ball_point``'s ``d**2 <= r*r`` test) instead
+    of the ``idw_neighbors`` nearest; same weights ``1/(d**idw_power + 1e-10)``; a voxel with no
+    particle in its ball is NaN.  Parity unpinned (the reference has no radius search); tested
+    against ``oracle.cpu_ref.idw_radius_points`` to 1e-12 normwise.
     """
     X, Y, Z = grid_tuple
     points = np.asarray(df[["x", "y", "z"]].values, dtype=np.float64)
@@ -240,6 +259,9 @@ def interpolate_field(df, grid_tuple, method="linear", rbf_neighbors=20, rbf_ker
     if method == "sibson":
         print(f"Using Sibson (Natural Neighbor) Interpolation (neighbors={sibson_neighbors})...")
         return _knn_field(points, values, grid_tuple, "sibson", int(sibson_neighbors), 2.0)
+    if method == "idw" and idw_radius is not None:
+        print(f"Using IDW Interpolation (power={idw_power}, radius={idw_radius})...")
+        return _knn_field(points, values, grid_tuple, "idw_radius", 1, float(idw_power), float(idw_radius))
     if method == "idw":
         print(f"Using IDW Interpolation (power={idw_power}, neighbors={idw_neighbors})...")
         return _knn_field(points, values, grid_tuple, "idw", int(idw_neighbors), float(idw_power))

@@ -155,3 +155,23 @@ def test_oracle_rgi_nearest_tie_and_bounds():
     assert cpu_ref.rgi_nearest_index(g, x).tolist() == [-1, 0, 0, 1, 1, 3, 3, -1]
     assert cpu_ref.rgi_nearest_index(g[::-1], x).tolist() == [-1, 3, 3, 2, 2, 0, 0, -1]
     assert cpu_ref.rgi_nearest_index(np.array([2.0]), np.array([2.0, 2.5])).tolist() == [0, -1]
+
+
+def test_idw_radius_oracle_matches_bruteforce():
+    """The fixed-radius IDW restatement (an extension; parity unpinned) against a brute-force
+    evaluation of its definition: d2 <= r*r, w = 1/(d**p + 1e-10), sum(w v)/sum(w), NaN if empty."""
+    rng = np.random.default_rng(5)
+    P = rng.uniform(0, 10, (500, 3))
+    Q = rng.standard_normal((500, 3))
+    q = rng.uniform(0, 10, (300, 3))
+    for r, p in ((1.0, 2.0), (2.5, 1.5), (0.3, 2.0)):
+        got = cpu_ref.idw_radius_points(P, Q, q, r, power=p)
+        for i in range(len(q)):
+            dd = q[i] - P
+            d2 = (dd[:, 0] * dd[:, 0] + dd[:, 1] * dd[:, 1]) + dd[:, 2] * dd[:, 2]
+            sel = d2 <= r * r
+            if not sel.any():
+                assert np.isnan(got[i]).all()
+                continue
+            w = 1.0 / (np.sqrt(d2[sel]) ** p + 1e-10)
+            np.testing.assert_allclose(got[i], (w[:, None] * Q[sel]).sum(0) / w.sum(), rtol=1e-13, atol=1e-15)
