@@ -723,7 +723,8 @@ def main_div(args):
 
 def main_filter(args):
     """--method filter: one step = remove_outliers_knn (filtering.py:5-58) over a resident particle set:
-    binning + (k+1)-NN of every particle among the particles (slot mode) + median/MAD per particle.
+    binning + (k+1)-NN of every particle among the particles with the median/MAD statistics fused
+    into the search kernel's epilogue (filter mode).
     Weak scaling: each rank filters its own sphere-pack copy (independent particle sets)."""
     import torch
 
@@ -781,9 +782,9 @@ def main_filter(args):
             "breakdown_ms": {"bin": round(st["ms_bin"], 3), "knn+stats": round(kavg, 3)},
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(ach / HBM_PEAK_GBPS, 4),
-                         "traffic": row_traffic("filter:k_knn_interp", "filter:k_outlier_stats")
+                         "traffic": row_traffic("filter:k_knn_interp", "filter:k_slot_speed")
                          if (k == 25 and n == 5_000_000) else None,
-                         "kernel": f"k_knn_interp<{32 if k + 1 <= 32 else 64}> (slot mode) + k_outlier_stats",
+                         "kernel": f"k_knn_interp<{kmax_for(k + 1)}, filter> ((k+1)-NN + fused median/MAD)",
                          "alg_bytes_per_launch": alg, "kernel_ms": round(kavg, 4)},
             "cpu_baseline": cpu}), flush=True)
     ctx.close()

@@ -83,7 +83,7 @@ struct ptv_ctx {
     DevBuf<double> bnd_xyz;                                      // boundary host calls: coordinates
     DevBuf<uint8_t> flt_keep;                                    // outlier filter host calls
     DevBuf<uint32_t> flt_code, flt_perm, flt_count, flt_start, flt_scanp;  // filter: Morton keys/ids, sort temp
-    DevBuf<double> flt_kth;
+    DevBuf<double> flt_kth, flt_spd;
     DevBuf<double> cull[6], cull_win;                            // slab cull: kept particles, z window
     DevBuf<uint32_t> cull_cnt;                                   // slab cull: per-block counts
     DevBuf<unsigned long long> halo_need;                        // slab cull: proven halo (double bits)
@@ -217,6 +217,7 @@ int ptv_free(ptv_ctx *c) {
     c->flt_keep.release();
     for (auto *b : {&c->flt_code, &c->flt_perm, &c->flt_count, &c->flt_start, &c->flt_scanp}) b->release();
     c->flt_kth.release();
+    c->flt_spd.release();
     for (auto &b : c->cull) b.release();
     c->cull_win.release();
     c->cull_cnt.release();
@@ -1361,24 +1362,32 @@ int run_filter(ptv_ctx *c, const ptv_particles *p, const ptv_filter_params *prm,
     const double lo[3] = {c->h_bbox[0], c->h_bbox[1], c->h_bbox[2]};
     const double hi[3] = {c->h_bbox[3], c->h_bbox[4], c->h_bbox[5]};
     const size_t tb = morton_sort_temp_bytes(n);
-    PTV_TRY(c->flt_code.ensure(n));
+    PTV_TRY(c->flt_code.ensure((size_t)npad));  // Morton keys, then the queries' original indices
     PTV_TRY(c->flt_count.ensure(n));
     PTV_TRY(c->flt_start.ensure(n));
     PTV_TRY(c->flt_perm.ensure(n));
     PTV_TRY(c->flt_scanp.ensure(tb / 4 + 1));
     PTV_TRY(launch_morton_order(p->x, p->y, p->z, n, lo, hi, c->flt_code.p, c->flt_count.p, c->flt_start.p,
                                 c->flt_perm.p, c->flt_scanp.p, tb, s));
+    // q_orig: the original index at each query position (reuses the Morton key buffer, dead
+    // after the sort); the speeds of the binned particles in slot order
+    uint32_t *q_orig = c->flt_code.p;
     PTV_TRY(launch_query_layout(c->flt_perm.p, p->x, p->y, p->z, n, npad, c->qpts[0].p, c->qpts[1].p, c->qpts[2].p,
-                                s));
-    PTV_TRY(c->slots.ensure((size_t)npad * (prm->k + 1)));
-    kl.mode = kModeSlots;
-    kl.slots = c->slots.p;
+                                q_orig, s));
+    PTV_TRY(c->flt_spd.ensure((size_t)n));
+    PTV_TRY(launch_slot_speed(b.pval, n, c->flt_spd.p, s));
+    // the (k+1)-NN search with the statistics fused into its epilogue (no slot list in HBM)
+    kl.mode = kModeFilter;
+    kl.fe.q_orig = q_orig;
+    kl.fe.inv = c->code.p;  // the binning's inverse permutation (launch_bin: code = inv after the scatter)
+    kl.fe.spd = c->flt_spd.p;
+    kl.fe.keep = keep;
+    kl.fe.kth = kth;
+    kl.fe.threshold = prm->threshold;
+    kl.fe.mad_eps = prm->mad_eps;
     c->rbf_chunks = 0;
     PTV_TRY(launch_knn(kl, b, nullptr, nullptr, nullptr, c->qpts[0].p, c->qpts[1].p, c->qpts[2].p, nullptr, nullptr,
                        nullptr, nullptr, s));
-    FilterArgs fa{n, prm->k, prm->threshold, prm->mad_eps};
-    const ParticleCols pc{p->x, p->y, p->z, p->u, p->v, p->w};
-    PTV_TRY(launch_outlier_stats(fa, b, c->flt_perm.p, pc, c->slots.p, keep, kth, s));
     PTV_HIP(hipEventRecord(c->ev_knn1, s));
     c->timed_pending = true;
     c->last.n_voxels = n;

@@ -14,12 +14,15 @@
 // wave tile of 64 is then laid out like a 4x4x4 voxel tile: the 8 queries of Morton
 // sub-group s go to the lanes whose bits (1, 3, 5) spell s, which is how the k-NN kernel
 // groups lanes into its 8 sub-balls (ptv_knn.hip), so the sub-ball candidate filter
-// works on particle queries too.  This file holds the kernels either side of the search:
-// the Morton sort and query layout, and the per-particle statistics.
+// works on particle queries too.  The per-particle statistics (speeds of the k neighbours,
+// median, MAD, keep test) run in the search kernel's epilogue (kModeFilter, ptv_knn.hip), so
+// no neighbour list goes through HBM.  This file holds the kernels before the search: the
+// Morton sort, the query layout and the slot-order speeds.
 #include <hipcub/hipcub.hpp>
 
 #include "ptv_api.h"
 #include "ptv_kernels.hpp"
+#include "ptv_median.hpp"
 
 namespace ptv {
 
@@ -93,11 +96,12 @@ __device__ __forceinline__ int64_t pos_of(int64_t g, int l) {
 }
 
 // position of tile g / lane l holds Morton query 64 g + query_of_lane(l) (the last particle
-// pads the final tiles)
+// pads the final tiles); q_orig[position] = the query's original index (~0 for the pads)
 __global__ __launch_bounds__(256) void k_query_layout(const uint32_t *__restrict__ perm, const double *__restrict__ x,
                                                       const double *__restrict__ y, const double *__restrict__ z,
                                                       int64_t n, int64_t npad, double *__restrict__ qx,
-                                                      double *__restrict__ qy, double *__restrict__ qz) {
+                                                      double *__restrict__ qy, double *__restrict__ qz,
+                                                      uint32_t *__restrict__ q_orig) {
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (tile, lane) = (t / 64, t % 64)
     if (t >= npad) return;
     const int64_t q = (t & ~(int64_t)63) + query_of_lane((int)(t & 63));
@@ -106,105 +110,20 @@ __global__ __launch_bounds__(256) void k_query_layout(const uint32_t *__restrict
     qx[p] = x[src];
     qy[p] = y[src];
     qz[p] = z[src];
+    if (q_orig) q_orig[p] = q < n ? src : 0xffffffffu;
 }
 
-// value at sorted position `pos` of s[0..n): the element whose [#less, #less-or-equal) holds pos
-template <int KMAX>
-__device__ __forceinline__ double select_pos(const double (&s)[KMAX], int n, int pos) {
-    double out = 0.0;
-#pragma unroll
-    for (int j = 0; j < KMAX; ++j) {
-        if (j < n) {
-            int lt = 0, le = 0;
-#pragma unroll
-            for (int i = 0; i < KMAX; ++i) {
-                if (i < n) {
-                    lt += s[i] < s[j] ? 1 : 0;
-                    le += s[i] <= s[j] ? 1 : 0;
-                }
-            }
-            if (lt <= pos && pos < le) out = s[j];
-        }
-    }
-    return out;
+// speed of every binned particle, slot order (filtering.py:16-17)
+__global__ __launch_bounds__(256) void k_slot_speed(const double4 *__restrict__ pval, int64_t n,
+                                                    double *__restrict__ spd) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) spd[i] = speed_of(pval[i]);
 }
 
-// np.median of n values (n odd: the middle one; n even: mean of the two middle ones, i.e.
-// (a + b) / 2); any NaN gives NaN (numpy's _median_nancheck)
-template <int KMAX>
-__device__ __forceinline__ double median_of(const double (&s)[KMAX], int n) {
-    bool nan = false;
-#pragma unroll
-    for (int j = 0; j < KMAX; ++j)
-        if (j < n) nan = nan || (s[j] != s[j]);
-    if (nan) return __longlong_as_double(0x7ff8000000000000LL);
-    if (n & 1) return select_pos(s, n, n >> 1);
-    const double a = select_pos(s, n, (n >> 1) - 1), b = select_pos(s, n, n >> 1);
-    return (a + b) / 2.0;
-}
-
-__device__ __forceinline__ double speed_of(const double4 v) {
-    return sqrt((v.x * v.x + v.y * v.y) + v.z * v.z);  // u**2 + v**2 + w**2, left to right
-}
-
-// one particle (binned order) per lane: its k+1 neighbour slots -> keep flag and the
-// distance to the (k+1)-th neighbour, written at the particle's original index
-template <int KMAX>
-__global__ __launch_bounds__(256) void k_outlier_stats(FilterArgs a, const double4 *__restrict__ prec,
-                                                       const double4 *__restrict__ pval,
-                                                       const uint32_t *__restrict__ perm, ParticleCols pc,
-                                                       const uint32_t *__restrict__ slots, uint8_t *__restrict__ keep,
-                                                       double *__restrict__ kth) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // Morton rank of the query
-    if (i >= a.n) return;
-    const int k1 = a.k + 1;
-    const uint32_t orig = perm[i];
-    const double4 q = make_double4(pc.x[orig], pc.y[orig], pc.z[orig], (double)orig);
-    const int64_t pos = pos_of(i >> 6, lane_of_query((int)(i & 63)));
-    const uint32_t *sl = slots + (size_t)pos * k1;
-    // the point itself is column 0 of the reference query (distance 0); when several
-    // particles coincide with it, the query point's own record is the one dropped
-    int drop = -1;
-    double dmin = INFINITY, dmax = 0.0;
-    int self = -1;
-#pragma unroll
-    for (int j = 0; j < KMAX + 1; ++j) {
-        if (j < k1) {
-            const uint32_t s = sl[j];
-            const double4 r = prec[s];
-            const double dx = r.x - q.x, dy = r.y - q.y, dz = r.z - q.z;
-            const double d = sqrt((dx * dx + dy * dy) + dz * dz);  // cKDTree p=2 accumulation
-            if (d < dmin) {
-                dmin = d;
-                drop = j;
-            }
-            dmax = fmax(dmax, d);
-            if (r.w == q.w) self = j;  // the same particle (original index)
-        }
-    }
-    if (self >= 0) drop = self;  // at distance 0 == dmin whenever it is in the list
-    double sp[KMAX];
-#pragma unroll
-    for (int t = 0; t < KMAX; ++t) sp[t] = 0.0;
-    int m = 0;
-#pragma unroll
-    for (int j = 0; j < KMAX + 1; ++j) {
-        if (j < k1 && j != drop) {
-            const double v = speed_of(pval[sl[j]]);
-#pragma unroll
-            for (int t = 0; t < KMAX; ++t)
-                if (t == m) sp[t] = v;
-            ++m;
-        }
-    }
-    const double med = median_of(sp, a.k);
-    double dev[KMAX];
-#pragma unroll
-    for (int t = 0; t < KMAX; ++t) dev[t] = fabs(sp[t] - med);
-    const double mad = median_of(dev, a.k);
-    const double z = fabs(speed_of(make_double4(pc.u[orig], pc.v[orig], pc.w[orig], 0.0)) - med) / (mad + a.mad_eps);
-    keep[orig] = z <= a.threshold ? 1 : 0;
-    if (kth) kth[orig] = dmax;
+int launch_slot_speed(const double4 *pval, int64_t n, double *spd, hipStream_t s) {
+    hipLaunchKernelGGL(k_slot_speed, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, pval, n, spd);
+    PTV_HIP(hipGetLastError());
+    return PTV_OK;
 }
 
 int filter_kmax(int k) {
@@ -256,25 +175,9 @@ int launch_morton_order(const double *x, const double *y, const double *z, int64
 }
 
 int launch_query_layout(const uint32_t *perm, const double *x, const double *y, const double *z, int64_t n,
-                        int64_t npad, double *qx, double *qy, double *qz, hipStream_t s) {
+                        int64_t npad, double *qx, double *qy, double *qz, uint32_t *q_orig, hipStream_t s) {
     hipLaunchKernelGGL(k_query_layout, dim3((unsigned)((npad + 255) / 256)), dim3(256), 0, s, perm, x, y, z, n, npad,
-                       qx, qy, qz);
-    PTV_HIP(hipGetLastError());
-    return PTV_OK;
-}
-
-int launch_outlier_stats(const FilterArgs &a, const Binned &b, const uint32_t *perm, const ParticleCols &pc,
-                         const uint32_t *slots, uint8_t *keep, double *kth, hipStream_t s) {
-    const dim3 grid((unsigned)((a.n + 255) / 256));
-    switch (filter_kmax(a.k)) {
-        case 8: hipLaunchKernelGGL(k_outlier_stats<8>, grid, dim3(256), 0, s, a, b.prec, b.pval, perm, pc, slots, keep, kth); break;
-        case 16: hipLaunchKernelGGL(k_outlier_stats<16>, grid, dim3(256), 0, s, a, b.prec, b.pval, perm, pc, slots, keep, kth); break;
-        case 32: hipLaunchKernelGGL(k_outlier_stats<32>, grid, dim3(256), 0, s, a, b.prec, b.pval, perm, pc, slots, keep, kth); break;
-        case 64: hipLaunchKernelGGL(k_outlier_stats<64>, grid, dim3(256), 0, s, a, b.prec, b.pval, perm, pc, slots, keep, kth); break;
-        default:
-            set_error("outlier filter: k must be <= 63 (k + 1 neighbours on the GPU k-NN list)");
-            return PTV_E_UNSUPPORTED;
-    }
+                       qx, qy, qz, q_orig);
     PTV_HIP(hipGetLastError());
     return PTV_OK;
 }

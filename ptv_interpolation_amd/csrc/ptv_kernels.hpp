@@ -45,6 +45,17 @@ constexpr int kModeInterp = 0;  // write U, V, W
 constexpr int kModeKDist = 1;   // write the exact k-th neighbour distance into U
 constexpr int kModeSlots = 2;   // write each voxel's k neighbour slots (sorted-record indices)
 constexpr int kModeRadius = 3;  // IDW over every particle within a fixed radius (PTV_METHOD_IDW_RADIUS)
+constexpr int kModeFilter = 4;  // the outlier filter's (k+1)-NN + median/MAD epilogue (filtering.py:20-51)
+
+// kModeFilter inputs / outputs (point-list queries = the particles, ptv_filter.hip layout)
+struct FilterEpilogue {
+    const uint32_t *q_orig = nullptr;  // original index of the query at each position (~0: pad)
+    const uint32_t *inv = nullptr;     // binning: slot of each original index
+    const double *spd = nullptr;       // speed of each binned particle (slot order)
+    uint8_t *keep = nullptr;           // keep flag per original index
+    double *kth = nullptr;             // distance to the (k+1)-th neighbour per original index (or NULL)
+    double threshold = 3.0, mad_eps = 1e-6;
+};
 
 struct KnnLaunch {
     CellGrid cg;
@@ -62,6 +73,7 @@ struct KnnLaunch {
     int lz0 = -1;                // plane of lattice point 0 (-1: z0); chunked launches keep the slab's
     uint32_t *slots = nullptr;   // kModeSlots: (z1 - z0, ny, nx, k) neighbour slots out
     double radius = 0.0;         // kModeRadius: the search radius
+    FilterEpilogue fe;           // kModeFilter
     const int *order = nullptr;  // dispatch order of the launch's blocks (NULL: XCD-contiguous ranges)
 };
 
@@ -167,30 +179,21 @@ int launch_boundary_emit(const BoundaryLaunch &m, const uint8_t *grown, const un
                          double *ox, double *oy, double *oz, hipStream_t s);
 
 // ---- k-NN outlier filter (ptv_filter.hip) ----
-struct FilterArgs {
-    int64_t n;
-    int k;               // neighbours without the point itself
-    double threshold;
-    double mad_eps;
-};
 int filter_kmax(int k);
 int launch_pad_queries(const double *x, const double *y, const double *z, int64_t n, int64_t npad, double *qx,
                        double *qy, double *qz, hipStream_t s);
 int launch_binned_queries(const double4 *prec, int64_t n, int64_t npad, double *qx, double *qy, double *qz,
                           hipStream_t s);
-struct ParticleCols {
-    const double *x, *y, *z, *u, *v, *w;  // original order
-};
 size_t morton_sort_temp_bytes(int64_t n);
 // perm = particle indices sorted by a 30-bit Morton code over [lo, hi] (stable)
 int launch_morton_order(const double *x, const double *y, const double *z, int64_t n, const double lo[3],
                         const double hi[3], uint32_t *keys, uint32_t *keys_out, uint32_t *ids, uint32_t *perm,
                         void *temp, size_t temp_bytes, hipStream_t s);
-// point-list query arrays (npad) in the sub-ball lane layout of the Morton order
+// speed sqrt((u^2 + v^2) + w^2) of every binned particle in slot order
+int launch_slot_speed(const double4 *pval, int64_t n, double *spd, hipStream_t s);
+// point-list query arrays (npad) in the sub-ball lane layout of the Morton order, and the
+// original index of the query at each position (q_orig, ~0 for the pads)
 int launch_query_layout(const uint32_t *perm, const double *x, const double *y, const double *z, int64_t n,
-                        int64_t npad, double *qx, double *qy, double *qz, hipStream_t s);
-// perm: Morton order of the queries; slots at the laid-out positions
-int launch_outlier_stats(const FilterArgs &a, const Binned &b, const uint32_t *perm, const ParticleCols &pc,
-                         const uint32_t *slots, uint8_t *keep, double *kth, hipStream_t s);
+                        int64_t npad, double *qx, double *qy, double *qz, uint32_t *q_orig, hipStream_t s);
 
 }  // namespace ptv

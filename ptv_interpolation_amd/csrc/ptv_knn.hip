@@ -40,6 +40,7 @@
 
 #include "../../include/ptv_api.h"
 #include "ptv_kernels.hpp"
+#include "ptv_median.hpp"
 #include "ptv_wave.hpp"
 
 namespace ptv {
@@ -83,6 +84,7 @@ struct KnnKernelArgs {
     int seed_n;        // seed records used per lattice corner (<= k)
     int nblocks;       // workgroups of the launch (the grid may be 2-D, see launch_knn)
     double radius;     // kModeRadius: every particle with d2 <= radius^2 (query_ball_point's test)
+    FilterEpilogue fe;  // kModeFilter
     const int *order;  // block dispatch order (NULL: XCD-contiguous ranges)
 };
 
@@ -908,6 +910,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
         write_stamps();
         return;
     }
+    if constexpr (MODE == kModeFilter) {
+        // remove_outliers_knn (filtering.py:20-51) for the query particle of this lane: its k+1
+        // nearest (the list, slots kpad..KMAX-1, ascending), minus "the point itself" (column 0
+        // of the reference's query: the query's own record when it is in the list, the nearest
+        // otherwise), the neighbours' speeds, median and MAD, the keep test, and the (k+1)-th
+        // distance (printed median, :33-35)
+        const uint32_t orig = a.fe.q_orig[vfull];
+        if (!active || orig == 0xffffffffu) return;
+        const uint32_t qslot = a.fe.inv[orig];
+        const double dk1 = sqrt(bd[KMAX - 1]);  // the (k+1)-th distance
+        // left-shift the list by kpad (uniform) so the k+1 entries occupy slots 0..k
+#pragma unroll
+        for (int sh = 1; sh < KMAX; sh <<= 1) {
+            if (a.kpad & sh) {
+#pragma unroll
+                for (int j = 0; j + sh < KMAX; ++j) bp[j] = bp[j + sh];
+            }
+        }
+        const int k1 = a.k, kk = a.k - 1;  // k1 = k + 1 listed, kk = k neighbours without the point
+        int drop = 0;
+        double v[KMAX];
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+            if (j < k1 && (uint32_t)bp[j] == qslot) drop = j;
+            v[j] = j < k1 ? a.fe.spd[max(bp[j], 0)] : 0.0;  // every gather in flight together
+        }
+        double sp[KMAX];
+#pragma unroll
+        for (int t = 0; t < KMAX; ++t) sp[t] = t + 1 < KMAX ? (t < drop ? v[t] : v[t + 1]) : 0.0;
+        const double med = median_of(sp, kk);
+        double dev[KMAX];
+#pragma unroll
+        for (int t = 0; t < KMAX; ++t) dev[t] = fabs(sp[t] - med);
+        const double mad = median_of(dev, kk);
+        const double zsc = fabs(a.fe.spd[qslot] - med) / (mad + a.fe.mad_eps);
+        a.fe.keep[orig] = zsc <= a.fe.threshold ? 1 : 0;
+        if (a.fe.kth != nullptr) a.fe.kth[orig] = dk1;
+        return;
+    }
     if constexpr (MODE == kModeSlots) {
         // the k neighbour slots (list order) for the local-RBF solve (ptv_rbf.hip)
         if (!active) return;
@@ -1263,6 +1304,9 @@ static void launch_t(dim3 grid, hipStream_t s, const KnnKernelArgs &ka, const Bi
         case kModeRadius:
             if constexpr (KMAX == 4) launch_m<KMAX, kModeRadius>(grid, s, ka, b, ax, ay, az, qx, qy, qz, mask, U, V, W);
             break;
+        case kModeFilter:
+            if constexpr (KMAX >= 4) launch_m<KMAX, kModeFilter>(grid, s, ka, b, ax, ay, az, qx, qy, qz, mask, U, V, W);
+            break;
         default: launch_m<KMAX, kModeInterp>(grid, s, ka, b, ax, ay, az, qx, qy, qz, mask, U, V, W);
     }
 }
@@ -1301,6 +1345,12 @@ int launch_knn(const KnnLaunch &a, const Binned &b, const double *ax, const doub
     ka.lz0 = a.lz0 < 0 ? a.z0 : a.lz0;
     ka.slots = a.slots;
     ka.radius = a.radius;
+    ka.fe = a.fe;
+    if (a.mode == kModeFilter && (a.fe.q_orig == nullptr || a.fe.inv == nullptr || a.fe.spd == nullptr ||
+                                  a.fe.keep == nullptr || a.k < 2)) {
+        set_error("filter-mode k-NN launch needs its epilogue buffers and k + 1 >= 2");
+        return PTV_E_ARG;
+    }
     if (a.mode == kModeRadius && !(a.radius > 0.0 && a.radius < INFINITY)) {
         set_error("radius search needs a positive finite radius");
         return PTV_E_ARG;

@@ -14,7 +14,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = {"filter": ["k_knn_interp", "k_outlier_stats"], "mask": ["k_mask_sample_sep", "k_boundary_count16",
+KERNELS = {"filter": ["k_knn_interp", "k_slot_speed"], "mask": ["k_mask_sample_sep", "k_boundary_count16",
                                                                    "k_boundary_emit16"],
            "div": ["k_divergence"]}
 
