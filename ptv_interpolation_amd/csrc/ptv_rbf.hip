@@ -65,6 +65,16 @@ __device__ __forceinline__ double elim_multiplier(double a, double p) {
     return ap >= DBL_MIN ? a * (1.0 / p) : a / p;
 }
 
+// 1/p for the SPD kernels' multipliers l = a * (1/p) (LAPACK dgetf2's reciprocal scaling),
+// branch-free: the Newton reciprocal where it is valid, IEEE division otherwise (an infinite or
+// subnormal pivot; a branch here made the 16-lane kernel's unrolled elimination spill)
+__device__ __forceinline__ double spd_recip(double p) {
+    const double ap = fabs(p);
+    const double q = 1.0 / p;
+    const double r = rcp_nr(p);
+    return (ap > 0x1p-1020 && ap < 0x1p1020) ? r : q;
+}
+
 __device__ __forceinline__ void rbf_wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -586,7 +596,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PTV_RBF_SPD
         rbf_wave_sync();
         const double piv = prow[c];
         singular = singular || piv == 0.0;
-        const double l = (li > c && li < M && piv != 0.0) ? elim_multiplier(A[c], piv) : 0.0;
+        const double rp = spd_recip(piv);
+        const double l = (li > c && li < M && piv != 0.0) ? A[c] * rp : 0.0;
 #pragma unroll
         for (int j = c + 1; j < M; ++j) A[j] = fma(-l, prow[j], A[j]);
         b0 = fma(-l, prow[M], b0);
@@ -660,6 +671,263 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PTV_RBF_SPD
     W[vo] = o2;
 }
 
+// ---------------------------------------------------------------------------
+// SPD systems, register-only factorisation: four systems per wave, one per 16-lane row, lane
+// li holding rows li and li + 16 (R = 2 for M <= 32).  Every broadcast of the elimination and
+// the back substitution is the DPP row_newbcast of the pivot lane's register
+// (v_mov_b64_dpp row_newbcast:n, within each 16-lane row): no LDS round trip, no barrier.
+// The LDS-broadcast kernel above was LDS-issue bound (SQ_WAIT_INST_LDS 35 % of wave cycles,
+// one 8-cycle ds_read_b128 per two pivot-row values).  Same arithmetic and order as k_rbf_spd
+// (no pivoting, fma updates, the multiplier a * spd_recip(p)), so the two agree bit for bit.
+// ---------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ double rowbcast(double v) {  // lane N of this lane's 16-lane row
+    return __longlong_as_double(
+        __builtin_amdgcn_update_dpp(0LL, __double_as_longlong(v), 0x150 + N, 0xF, 0xF, false));
+}
+
+// the same with a lane index that the unrolled loops fold to a constant (the DPP control must be one)
+__device__ __forceinline__ double rowbcast_n(int n, double v) {
+    switch (n & 15) {
+        case 0: return rowbcast<0>(v);
+        case 1: return rowbcast<1>(v);
+        case 2: return rowbcast<2>(v);
+        case 3: return rowbcast<3>(v);
+        case 4: return rowbcast<4>(v);
+        case 5: return rowbcast<5>(v);
+        case 6: return rowbcast<6>(v);
+        case 7: return rowbcast<7>(v);
+        case 8: return rowbcast<8>(v);
+        case 9: return rowbcast<9>(v);
+        case 10: return rowbcast<10>(v);
+        case 11: return rowbcast<11>(v);
+        case 12: return rowbcast<12>(v);
+        case 13: return rowbcast<13>(v);
+        case 14: return rowbcast<14>(v);
+        default: return rowbcast<15>(v);
+    }
+}
+
+constexpr int kSpd16Cols = 8;  // build columns per LDS round
+
+template <int M, int KERN>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_rbf_spd16(
+    RbfKernelArgs a, const double4 *__restrict__ prec, const double4 *__restrict__ pval,
+    const uint32_t *__restrict__ slots, const double *__restrict__ ax, const double *__restrict__ ay,
+    const double *__restrict__ az, const double *__restrict__ qpx, const double *__restrict__ qpy,
+    const double *__restrict__ qpz, const uint8_t *__restrict__ mask, double *__restrict__ U,
+    double *__restrict__ V, double *__restrict__ W, int *__restrict__ status) {
+    static_assert(M <= 32, "two rows per lane");
+    constexpr int R = (M + 15) / 16;  // rows per lane
+    __shared__ double4 s_ye[4][4][32];  // per wave and system: eps-scaled coordinates + id, id order
+    // per wave: the sorted values and ids, then the build scratch [row set][column][lane]
+    constexpr int SC = R * kSpd16Cols * 64 > 4 * 32 * 4 + 4 * 32 / 2 ? R * kSpd16Cols * 64 : 4 * 32 * 4 + 4 * 32 / 2;
+    __shared__ double s_sc[4][SC];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int seg = lane >> 4, li = lane & 15;
+    double4 *ye = s_ye[wid][seg];
+    double *sc = s_sc[wid];
+    double4 *sv = reinterpret_cast<double4 *>(sc) + seg * 32;
+    uint32_t *sid = reinterpret_cast<uint32_t *>(sc + 4 * 32 * 4) + seg * 32;
+
+    const long long plane = (long long)a.nx * a.ny;
+    const long long nvox = (long long)(a.z1 - a.z0) * plane;
+    const long long v = ((long long)blockIdx.x * 4 + wid) * 4 + seg;  // chunk-local voxel
+    const bool valid = v < nvox;
+    const long long vc = valid ? v : nvox - 1;
+    const int iz = a.z0 + (int)(vc / plane);
+    const long long rem = vc % plane;
+    const int iy = (int)(rem / a.nx), ix = (int)(rem % a.nx);
+    const size_t vfull = (size_t)iz * plane + rem;
+    const bool active = valid && (mask == nullptr || mask[vfull] != 0);
+    const int k = a.k;
+    const double eps = a.epsilon;
+
+    // ---- 1. neighbours li and li + 16, ranked by particle index (np.sort(yindices)) ----
+    double4 r[R], d[R];
+    uint32_t id[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        const int nbr = li + 16 * q;
+        r[q] = make_double4(0.0, 0.0, 0.0, 0.0);
+        d[q] = make_double4(0.0, 0.0, 0.0, 0.0);
+        id[q] = 0xffffffffu;
+        if (active && nbr < k) {
+            const uint32_t sl = slots[(size_t)v * k + nbr];
+            r[q] = prec[sl];
+            d[q] = pval[sl];
+            id[q] = (uint32_t)r[q].w;
+        }
+        if (nbr < 32) sid[nbr] = id[q];
+    }
+    rbf_wave_sync();
+    int rank[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) rank[q] = 0;
+    for (int j = 0; j < k; ++j) {
+        const uint32_t o = sid[j];
+#pragma unroll
+        for (int q = 0; q < R; ++q) rank[q] += (o < id[q] || (o == id[q] && j < li + 16 * q)) ? 1 : 0;
+    }
+    rbf_wave_sync();
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        if (li + 16 * q < k) {
+            ye[rank[q]] = make_double4(r[q].x * eps, r[q].y * eps, r[q].z * eps, (double)id[q]);
+            sv[rank[q]] = d[q];
+        }
+    }
+    rbf_wave_sync();
+    double4 yi[R];
+    double B[R][3];
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        const int row = li + 16 * q;
+        const bool kr = row < k;
+        yi[q] = kr ? ye[row] : make_double4(0.0, 0.0, 0.0, 0.0);
+        const double4 dv = kr ? sv[row] : make_double4(0.0, 0.0, 0.0, 0.0);
+        B[q][0] = dv.x;
+        B[q][1] = dv.y;
+        B[q][2] = dv.z;
+    }
+    rbf_wave_sync();  // the values' LDS is the build scratch next
+
+    // ---- 2. rows li and li + 16, kSpd16Cols columns per LDS round (a rolled loop: one copy of phi) ----
+    const double diag = rbf_phi<KERN>(0.0) + a.smoothing;
+    double A[R][M];
+#pragma unroll
+    for (int g = 0; g < M; g += kSpd16Cols) {
+#pragma unroll 1
+        for (int jj = 0; jj < kSpd16Cols; ++jj) {
+            const int j = g + jj;
+            const double4 yj = ye[min(j, 31)];
+#pragma unroll
+            for (int q = 0; q < R; ++q) {
+                const int row = li + 16 * q;
+                double e;
+                if (row < k && j < k) {
+                    const double dx = yi[q].x - yj.x, dy = yi[q].y - yj.y, dz = yi[q].z - yj.z;
+                    e = j == row ? diag : rbf_phi<KERN>(sqrt((dx * dx + dy * dy) + dz * dz));
+                } else {
+                    e = j == row ? 1.0 : 0.0;  // identity padding up to M
+                }
+                sc[(q * kSpd16Cols + jj) * 64 + lane] = e;
+            }
+        }
+        // each lane reads back only its own column of the scratch: no cross-lane hazard
+#pragma unroll
+        for (int jj = 0; jj < kSpd16Cols; ++jj)
+#pragma unroll
+            for (int q = 0; q < R; ++q)
+                if (g + jj < M) A[q][g + jj] = sc[(q * kSpd16Cols + jj) * 64 + lane];
+    }
+
+    // ---- 3. elimination without pivoting; pivot row c = lane c % 16, row set c / 16 ----
+    bool singular = false;
+#pragma unroll
+    for (int c = 0; c < M; ++c) {
+        const int pq = c / 16;
+        // c is a constant in the unrolled loop, so the row_newbcast lane folds to one
+#define PTV_BC(X) rowbcast_n(c, X)
+        const double piv = PTV_BC(A[pq][c]);
+        singular = singular || piv == 0.0;
+        const double rp = spd_recip(piv);
+        double l[R];
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const int row = li + 16 * q;
+            l[q] = (row > c && row < M && piv != 0.0) ? A[q][c] * rp : 0.0;
+        }
+#pragma unroll
+        for (int j = c + 1; j < M; ++j) {
+            const double u = PTV_BC(A[pq][j]);
+#pragma unroll
+            for (int q = 0; q < R; ++q) A[q][j] = fma(-l[q], u, A[q][j]);
+        }
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const double u = PTV_BC(B[pq][t]);
+#pragma unroll
+            for (int q = 0; q < R; ++q) B[q][t] = fma(-l[q], u, B[q][t]);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep the steps apart (register pressure)
+    }
+
+    // ---- 4. back substitution: x_c = b_c / U_cc from lane c % 16; B becomes the solution ----
+    double rd[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        rd[q] = 1.0;
+#pragma unroll
+        for (int j = 0; j < M; ++j)
+            if (j == li + 16 * q) rd[q] = 1.0 / A[q][j];
+    }
+#pragma unroll
+    for (int c = M - 1; c >= 0; --c) {
+        const int pq = c / 16;
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const double xc = PTV_BC(B[pq][t] * rd[pq]);
+#pragma unroll
+            for (int q = 0; q < R; ++q) {
+                const int row = li + 16 * q;
+                if (row == c) B[q][t] = xc;  // row c's solution component
+                const double u = row < c ? A[q][c] : 0.0;
+                B[q][t] = fma(-u, xc, B[q][t]);
+            }
+        }
+    }
+#undef PTV_BC
+
+    // ---- 5. evaluate at the voxel: sum_j phi(eps |x - y_j|) c_j ----
+    double qx, qy, qz;
+    if (a.separable) {
+        qx = ax[ix];
+        qy = ay[iy];
+        qz = az[iz];
+    } else {
+        qx = qpx[vfull];
+        qy = qpy[vfull];
+        qz = qpz[vfull];
+    }
+    double o0 = 0.0, o1 = 0.0, o2 = 0.0;
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        double e = 0.0;
+        if (li + 16 * q < k) {
+            const double dx = qx * eps - yi[q].x, dy = qy * eps - yi[q].y, dz = qz * eps - yi[q].z;
+            e = rbf_phi<KERN>(sqrt((dx * dx + dy * dy) + dz * dz));
+        }
+        o0 += e * B[q][0];
+        o1 += e * B[q][1];
+        o2 += e * B[q][2];
+    }
+    o0 = seg_sum<16>(o0);
+    o1 = seg_sum<16>(o1);
+    o2 = seg_sum<16>(o2);
+    if (!valid || li != 0) return;
+    const size_t vo = (size_t)(iz - a.out_z0) * plane + rem;
+    if (!active) {
+        U[vo] = 0.0;
+        V[vo] = 0.0;
+        W[vo] = 0.0;
+        return;
+    }
+    if (singular) {
+        atomicAdd(&status[0], 1);
+        atomicMin(&status[1], (int)min((long long)vfull, 0x7fffffffLL));
+    }
+    if (a.flags & PTV_FLAG_NAN_TO_NUM) {
+        auto fix = [](double x) { return x != x ? 0.0 : (x == INFINITY ? DBL_MAX : (x == -INFINITY ? -DBL_MAX : x)); };
+        o0 = fix(o0);
+        o1 = fix(o1);
+        o2 = fix(o2);
+    }
+    U[vo] = o0;
+    V[vo] = o1;
+    W[vo] = o2;
+}
+
 template <int M, int KERN>
 static void launch_spd_t(const RbfKernelArgs &ka, long long nvox, hipStream_t s, const double4 *prec,
                          const double4 *pval, const uint32_t *slots, const double *ax, const double *ay,
@@ -696,7 +964,7 @@ static void launch_spd_m(const RbfKernelArgs &ka, long long nvox, hipStream_t s,
 // whether the system is symmetric positive definite (see k_rbf_spd) and of a size it serves
 static bool rbf_spd(const RbfKernelArgs &ka, const double *smooth) {
     if (const char *e = std::getenv("PTV_RBF_SPD"))  // dev knob: 0 = always the pivoting kernel
-        if (e[0] == '0') return false;
+        if (e[0] == '0') return false;  // (1 = the LDS-broadcast SPD kernel, see launch_rbf)
     const bool pd_kernel = ka.kernel == PTV_RBF_GAUSSIAN || ka.kernel == PTV_RBF_INVERSE_MULTIQUADRIC ||
                            ka.kernel == PTV_RBF_INVERSE_QUADRATIC;
     return pd_kernel && ka.m == ka.k && smooth == nullptr && ka.smoothing >= 0.0 && rbf_system_size(ka.m) <= 32;
@@ -737,6 +1005,28 @@ int launch_rbf(const RbfKernelArgs &ka, const Binned &b, const uint32_t *slots, 
         return PTV_E_ARG;
     }
     if (rbf_spd(ka, smooth)) {
+        const char *e = std::getenv("PTV_RBF_SPD");  // dev knob: 1 = the LDS-broadcast SPD kernel
+        if (!(e && e[0] == '1')) {
+            const long long waves = (nvox + 3) / 4;
+            const dim3 grid((unsigned)((waves + 3) / 4));
+#define PTV_S16(MM, KK) hipLaunchKernelGGL((k_rbf_spd16<MM, KK>), grid, dim3(256), 0, s, ka, b.prec, b.pval, slots, ax, ay, az, qx, qy, qz, mask, U, V, W, status)
+#define PTV_S16K(MM) \
+    switch (ka.kernel) { \
+        case PTV_RBF_INVERSE_MULTIQUADRIC: PTV_S16(MM, PTV_RBF_INVERSE_MULTIQUADRIC); break; \
+        case PTV_RBF_INVERSE_QUADRATIC: PTV_S16(MM, PTV_RBF_INVERSE_QUADRATIC); break; \
+        default: PTV_S16(MM, PTV_RBF_GAUSSIAN); \
+    }
+            switch (M) {
+                case 8: PTV_S16K(8) break;
+                case 16: PTV_S16K(16) break;
+                case 24: PTV_S16K(24) break;
+                default: PTV_S16K(32)
+            }
+#undef PTV_S16K
+#undef PTV_S16
+            PTV_HIP(hipGetLastError());
+            return PTV_OK;
+        }
         switch (M) {
             case 8: launch_spd_m<8>(ka, nvox, s, b.prec, b.pval, slots, ax, ay, az, qx, qy, qz, mask, U, V, W, status); break;
             case 16: launch_spd_m<16>(ka, nvox, s, b.prec, b.pval, slots, ax, ay, az, qx, qy, qz, mask, U, V, W, status); break;
