@@ -708,7 +708,6 @@ __device__ __forceinline__ double rowbcast_n(int n, double v) {
     }
 }
 
-constexpr int kSpd16Cols = 8;  // build columns per LDS round
 
 template <int M, int KERN>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_rbf_spd16(
@@ -720,8 +719,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     static_assert(M <= 32, "two rows per lane");
     constexpr int R = (M + 15) / 16;  // rows per lane
     __shared__ double4 s_ye[4][4][32];  // per wave and system: eps-scaled coordinates + id, id order
-    // per wave: the sorted values and ids, then the build scratch [row set][column][lane]
-    constexpr int SC = R * kSpd16Cols * 64 > 4 * 32 * 4 + 4 * 32 / 2 ? R * kSpd16Cols * 64 : 4 * 32 * 4 + 4 * 32 / 2;
+    // per wave: the sorted values and ids, then the symmetric build scratch (4 systems x 16R
+    // rows x 8R entries): 80 KB per block at R = 2, two blocks (the register budget's 2 waves
+    // per SIMD) per CU
+    constexpr int SC = 4 * (16 * R) * (8 * R) > 4 * 32 * 4 + 4 * 32 / 2 ? 4 * (16 * R) * (8 * R) : 4 * 32 * 4 + 4 * 32 / 2;
     __shared__ double s_sc[4][SC];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int seg = lane >> 4, li = lane & 15;
@@ -792,34 +793,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     }
     rbf_wave_sync();  // the values' LDS is the build scratch next
 
-    // ---- 2. rows li and li + 16, kSpd16Cols columns per LDS round (a rolled loop: one copy of phi) ----
+    // ---- 2. symmetric build of rows li and li + 16: row i evaluates phi for the columns
+    //      (i + d) mod NR, d = 1..H, into its segment's scratch (column swizzled by the row:
+    //      conflict-free stores); entry (i, j) is then its own (d = (j - i) mod NR <= H) or its
+    //      partner row j's (d' = NR - d).  H phi per row instead of k. ----
+    constexpr int NR = 16 * R, H = NR / 2;
+    double *ss = sc + seg * (NR * H);
     const double diag = rbf_phi<KERN>(0.0) + a.smoothing;
+#pragma unroll 1
+    for (int dd = 1; dd <= H; ++dd) {
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const int row = li + 16 * q;
+            const int j = (row + dd) & (NR - 1);
+            double e = 0.0;
+            if (row < k && j < k) {
+                const double4 yj = ye[j];
+                const double dx = yi[q].x - yj.x, dy = yi[q].y - yj.y, dz = yi[q].z - yj.z;
+                e = rbf_phi<KERN>(sqrt((dx * dx + dy * dy) + dz * dz));
+            }
+            ss[row * H + ((dd - 1) ^ (row & (H - 1)))] = e;
+        }
+    }
+    rbf_wave_sync();  // the partner rows' entries are read next
     double A[R][M];
 #pragma unroll
-    for (int g = 0; g < M; g += kSpd16Cols) {
-#pragma unroll 1
-        for (int jj = 0; jj < kSpd16Cols; ++jj) {
-            const int j = g + jj;
-            const double4 yj = ye[min(j, 31)];
+    for (int j = 0; j < M; ++j) {
 #pragma unroll
-            for (int q = 0; q < R; ++q) {
-                const int row = li + 16 * q;
-                double e;
-                if (row < k && j < k) {
-                    const double dx = yi[q].x - yj.x, dy = yi[q].y - yj.y, dz = yi[q].z - yj.z;
-                    e = j == row ? diag : rbf_phi<KERN>(sqrt((dx * dx + dy * dy) + dz * dz));
-                } else {
-                    e = j == row ? 1.0 : 0.0;  // identity padding up to M
-                }
-                sc[(q * kSpd16Cols + jj) * 64 + lane] = e;
-            }
+        for (int q = 0; q < R; ++q) {
+            const int row = li + 16 * q;
+            const int dj = (j - row) & (NR - 1);
+            const int addr = dj == 0 ? 0
+                             : (dj <= H ? row * H + ((dj - 1) ^ (row & (H - 1)))
+                                        : j * H + ((NR - dj - 1) ^ (j & (H - 1))));
+            const double e = ss[addr];
+            A[q][j] = (row >= k || j >= k) ? (j == row ? 1.0 : 0.0) : (dj == 0 ? diag : e);
         }
-        // each lane reads back only its own column of the scratch: no cross-lane hazard
-#pragma unroll
-        for (int jj = 0; jj < kSpd16Cols; ++jj)
-#pragma unroll
-            for (int q = 0; q < R; ++q)
-                if (g + jj < M) A[q][g + jj] = sc[(q * kSpd16Cols + jj) * 64 + lane];
+        if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // bounded reads in flight
     }
 
     // ---- 3. elimination without pivoting; pivot row c = lane c % 16, row set c / 16 ----
