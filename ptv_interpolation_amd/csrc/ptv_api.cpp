@@ -730,11 +730,10 @@ int run_rbf(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_rbf
     PTV_TRY(prepare(c, p, g, &sp, ax, ay, az, qx, qy, qz, s, kl, b));
     const std::vector<int> pw = monomial_powers(prm->degree);
     PTV_TRY(c->rbf_pw.ensure(pw.size() + 1));
-    PTV_TRY(c->rbf_status.ensure(2));
+    PTV_TRY(c->rbf_status.ensure(3));
     if (!pw.empty())
         PTV_HIP(hipMemcpyAsync(c->rbf_pw.p, pw.data(), pw.size() * sizeof(int), hipMemcpyHostToDevice, s));
-    const int st_init[2] = {0, 0x7fffffff};
-    PTV_HIP(hipMemcpyAsync(c->rbf_status.p, st_init, sizeof(st_init), hipMemcpyHostToDevice, s));
+    const int st_init[3] = {0, 0x7fffffff, 0};
 
     const int64_t plane = g->nx * g->ny;
     const int64_t z0 = g->z_begin, z1 = g->z_end;
@@ -763,6 +762,12 @@ int run_rbf(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_rbf
     ra.epsilon = prm->epsilon;
     ra.smoothing = prm->smoothing;
     ra.flags = prm->flags;
+    int st_out[3] = {0, 0, 0};
+    for (int pass = 0; pass < 2; ++pass) {
+    // pass 1 (rare): k_rbf_spd16 met a pivot its reciprocal does not serve; redo every chunk with
+    // the LDS-broadcast SPD kernel (same arithmetic plus the IEEE division for such pivots)
+    ra.spd_lds = pass;
+    PTV_HIP(hipMemcpyAsync(c->rbf_status.p, st_init, sizeof(st_init), hipMemcpyHostToDevice, s));
     for (int ch = 0; ch < nchunks; ++ch) {
         const int za = (int)(z0 + (int64_t)ch * cp), zb = (int)std::min<int64_t>(z1, za + cp);
         KnnLaunch cl = kl;
@@ -780,10 +785,11 @@ int run_rbf(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_rbf
                            c->rbf_status.p, s));
         PTV_HIP(hipEventRecord(c->rbf_ev[3 * ch + 2], s));
     }
-    c->rbf_chunks = nchunks;
-    int st_out[2] = {0, 0};
     PTV_HIP(hipMemcpyAsync(st_out, c->rbf_status.p, sizeof(st_out), hipMemcpyDeviceToHost, s));
     PTV_HIP(hipStreamSynchronize(s));
+    if (st_out[2] == 0) break;
+    }
+    c->rbf_chunks = nchunks;
     *n_singular = st_out[0];
     c->last.n_singular = st_out[0];
     if (st_out[0] > 0) {

@@ -137,13 +137,16 @@ struct RbfKernelArgs {
     double epsilon;
     double smoothing;  // scalar smoothing (when no per-particle array is given)
     uint32_t flags;
+    int spd_lds;       // SPD systems: the LDS-broadcast k_rbf_spd instead of k_rbf_spd16 (the
+                       // rerun after k_rbf_spd16 flagged an out-of-range pivot in status[2])
 };
 
 int rbf_system_size(int m);  // padded system size served, 0 if unsupported
 
 // slots: (z1 - z0, ny, nx, k) neighbour slots from launch_knn(kModeSlots); pw: the
 // monomial exponents (m - k entries, px | py << 8 | pz << 16); status[0] counts singular
-// systems, status[1] keeps the lowest singular voxel index.
+// systems, status[1] keeps the lowest singular voxel index, status[2] != 0 asks for a rerun
+// with spd_lds set.
 int launch_rbf(const RbfKernelArgs &ka, const Binned &b, const uint32_t *slots, const double *ax, const double *ay,
                const double *az, const double *qx, const double *qy, const double *qz, const double *smooth,
                const int *pw, const uint8_t *mask, double *U, double *V, double *W, int *status, hipStream_t s);

@@ -130,7 +130,9 @@ __device__ __forceinline__ double mono(double hx, double hy, double hz, int code
 // Every lane of the segment ends with the same value (each step combines symmetric pairs). ----
 template <int CTRL>
 __device__ __forceinline__ unsigned dpp_u32(unsigned v) {
-    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+    // bound_ctrl: every source lane of these patterns is valid, so no old value is needed
+    // (the compiler then drops the v_mov that would initialise it)
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, true);
 }
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v) {
@@ -607,10 +609,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PTV_RBF_SPD
 
     // ---- 4. back substitution: x_c = b_c / U_cc on lane c, broadcast through LDS (the
     //      pivot-row buffers, free now; double buffered, one barrier per step) ----
-    double rd = 1.0;
+    double dg = 1.0;
 #pragma unroll
     for (int j = 0; j < M; ++j)
-        if (j == li) rd = 1.0 / A[j];
+        if (j == li) dg = A[j];
+    const double rd = spd_recip(dg);  // = k_rbf_spd16's rcp_nr wherever that one is valid
     double x0 = 0.0, x1 = 0.0, x2 = 0.0;
 #pragma unroll
     for (int c = M - 1; c >= 0; --c) {
@@ -683,7 +686,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PTV_RBF_SPD
 template <int N>
 __device__ __forceinline__ double rowbcast(double v) {  // lane N of this lane's 16-lane row
     return __longlong_as_double(
-        __builtin_amdgcn_update_dpp(0LL, __double_as_longlong(v), 0x150 + N, 0xF, 0xF, false));
+        __builtin_amdgcn_update_dpp(0LL, __double_as_longlong(v), 0x150 + N, 0xF, 0xF, true));
 }
 
 // the same with a lane index that the unrolled loops fold to a constant (the DPP control must be one)
@@ -832,46 +835,67 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // bounded reads in flight
     }
 
-    // ---- 3. elimination without pivoting; pivot row c = lane c % 16, row set c / 16 ----
-    bool singular = false;
+    // ---- 3. elimination without pivoting; pivot row c = lane c % 16, row set c / 16.
+    //      Row set q is finished once c >= 16 q + 15 (all its rows are above the pivot): its
+    //      updates are skipped at compile time.  The next column's pivot and reciprocal are
+    //      formed inside this column's step, right after its update of column c + 1, so that
+    //      their dependent chain overlaps the remaining updates (look-ahead by one column). ----
+    //      The reciprocal is v_rcp_f64 + two Newton steps alone (rcp_nr): a pivot outside
+    //      (2^-1020, 2^1020) sets `slow`, and the host reruns the launch with k_rbf_spd, whose
+    //      spd_recip adds the IEEE division for exactly those pivots (rare: a NaN or infinite
+    //      input, or a condition number near 1e300).  Each lane keeps the reciprocal of its own
+    //      rows' pivots (rd) for the back substitution. ----
+    bool singular = false, slow = false;
+#define PTV_BC(X) rowbcast_n(c, X)
+    double piv, rp, rd[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) rd[q] = 1.0;
+    {
+        constexpr int c = 0;
+        piv = PTV_BC(A[0][0]);
+        rp = rcp_nr(piv);
+    }
 #pragma unroll
     for (int c = 0; c < M; ++c) {
         const int pq = c / 16;
         // c is a constant in the unrolled loop, so the row_newbcast lane folds to one
-#define PTV_BC(X) rowbcast_n(c, X)
-        const double piv = PTV_BC(A[pq][c]);
         singular = singular || piv == 0.0;
-        const double rp = spd_recip(piv);
+        const double ap = fabs(piv);
+        slow = slow | ((ap <= 0x1p-1020) & (piv != 0.0)) | !(ap < 0x1p1020);  // bitwise: no branches
+        rd[pq] = li == (c & 15) ? rp : rd[pq];
         double l[R];
 #pragma unroll
         for (int q = 0; q < R; ++q) {
             const int row = li + 16 * q;
-            l[q] = (row > c && row < M && piv != 0.0) ? A[q][c] * rp : 0.0;
+            l[q] = (16 * q + 15 > c && row > c && row < M && piv != 0.0) ? A[q][c] * rp : 0.0;
         }
+        double pivn = 0.0, rpn = 1.0;
 #pragma unroll
         for (int j = c + 1; j < M; ++j) {
             const double u = PTV_BC(A[pq][j]);
 #pragma unroll
-            for (int q = 0; q < R; ++q) A[q][j] = fma(-l[q], u, A[q][j]);
+            for (int q = 0; q < R; ++q)
+                if (16 * q + 15 > c) A[q][j] = fma(-l[q], u, A[q][j]);
+            if (j == c + 1) {
+                pivn = rowbcast_n(c + 1, A[(c + 1) / 16][c + 1]);
+                rpn = rcp_nr(pivn);
+            }
         }
 #pragma unroll
         for (int t = 0; t < 3; ++t) {
             const double u = PTV_BC(B[pq][t]);
 #pragma unroll
-            for (int q = 0; q < R; ++q) B[q][t] = fma(-l[q], u, B[q][t]);
+            for (int q = 0; q < R; ++q)
+                if (16 * q + 15 > c) B[q][t] = fma(-l[q], u, B[q][t]);
         }
+        piv = pivn;
+        rp = rpn;
         __builtin_amdgcn_sched_barrier(0);  // keep the steps apart (register pressure)
     }
 
-    // ---- 4. back substitution: x_c = b_c / U_cc from lane c % 16; B becomes the solution ----
-    double rd[R];
-#pragma unroll
-    for (int q = 0; q < R; ++q) {
-        rd[q] = 1.0;
-#pragma unroll
-        for (int j = 0; j < M; ++j)
-            if (j == li + 16 * q) rd[q] = 1.0 / A[q][j];
-    }
+    // ---- 4. back substitution: x_c = b_c * (1 / U_cc) from lane c % 16.  Row r's b no longer
+    //      changes after step r (only rows above c are updated), so every lane scales its own
+    //      rows once at the end instead of taking x_r by a select at step r. ----
 #pragma unroll
     for (int c = M - 1; c >= 0; --c) {
         const int pq = c / 16;
@@ -880,13 +904,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
             const double xc = PTV_BC(B[pq][t] * rd[pq]);
 #pragma unroll
             for (int q = 0; q < R; ++q) {
-                const int row = li + 16 * q;
-                if (row == c) B[q][t] = xc;  // row c's solution component
-                const double u = row < c ? A[q][c] : 0.0;
-                B[q][t] = fma(-u, xc, B[q][t]);
+                if (16 * q < c) {  // row set q has rows above c
+                    const double u = li + 16 * q < c ? A[q][c] : 0.0;
+                    B[q][t] = fma(-u, xc, B[q][t]);
+                }
             }
         }
     }
+#pragma unroll
+    for (int q = 0; q < R; ++q)
+#pragma unroll
+        for (int t = 0; t < 3; ++t) B[q][t] = B[q][t] * rd[q];
 #undef PTV_BC
 
     // ---- 5. evaluate at the voxel: sum_j phi(eps |x - y_j|) c_j ----
@@ -927,6 +955,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         atomicAdd(&status[0], 1);
         atomicMin(&status[1], (int)min((long long)vfull, 0x7fffffffLL));
     }
+    if (slow) atomicOr(&status[2], 1);  // the host reruns this launch with k_rbf_spd
     if (a.flags & PTV_FLAG_NAN_TO_NUM) {
         auto fix = [](double x) { return x != x ? 0.0 : (x == INFINITY ? DBL_MAX : (x == -INFINITY ? -DBL_MAX : x)); };
         o0 = fix(o0);
@@ -1016,7 +1045,7 @@ int launch_rbf(const RbfKernelArgs &ka, const Binned &b, const uint32_t *slots, 
     }
     if (rbf_spd(ka, smooth)) {
         const char *e = std::getenv("PTV_RBF_SPD");  // dev knob: 1 = the LDS-broadcast SPD kernel
-        if (!(e && e[0] == '1')) {
+        if (!(e && e[0] == '1') && !ka.spd_lds) {
             const long long waves = (nvox + 3) / 4;
             const dim3 grid((unsigned)((waves + 3) / 4));
 #define PTV_S16(MM, KK) hipLaunchKernelGGL((k_rbf_spd16<MM, KK>), grid, dim3(256), 0, s, ka, b.prec, b.pval, slots, ax, ay, az, qx, qy, qz, mask, U, V, W, status)

@@ -16,13 +16,19 @@ template <int CTRL, int ROWMASK = 0xF>
 __device__ __forceinline__ int dpp_i32(int old, int v) {
     return __builtin_amdgcn_update_dpp(old, v, CTRL, ROWMASK, 0xF, false);
 }
+// the same where every lane is written and an invalid source lane reads 0 (bound_ctrl): no
+// old value, so no v_mov to initialise one (quad_perm / mirror patterns, and row_shr into a sum)
+template <int CTRL>
+__device__ __forceinline__ int dpp0_i32(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, true);
+}
 
 // a lane's reduction partner for one step: DPP control (quad_perm xor 1 / xor 2,
 // row_half_mirror, row_mirror) or a bit-mode ds_swizzle xor
 template <int CTRL>
 __device__ __forceinline__ int partner_i32(int v) {
     if constexpr (CTRL >= 0x1000) return __builtin_amdgcn_ds_swizzle(v, CTRL - 0x1000);
-    else return dpp_i32<CTRL>(0, v);
+    else return dpp0_i32<CTRL>(v);
 }
 constexpr int kSwizzleXor4 = 0x1000 + ((4 << 10) | 0x1f);
 constexpr int kSwizzleXor8 = 0x1000 + ((8 << 10) | 0x1f);
@@ -116,10 +122,10 @@ struct OpAdd {
 // inclusive prefix sum / prefix max over the wave: row_shr 1, 2, 4, 8 inside each
 // 16-lane row, then row_bcast15 (into rows 1, 3) and row_bcast31 (into rows 2, 3)
 __device__ __forceinline__ int wave_incl_scan_add(int v) {
-    v += dpp_i32<0x111>(0, v);
-    v += dpp_i32<0x112>(0, v);
-    v += dpp_i32<0x114>(0, v);
-    v += dpp_i32<0x118>(0, v);
+    v += dpp0_i32<0x111>(v);
+    v += dpp0_i32<0x112>(v);
+    v += dpp0_i32<0x114>(v);
+    v += dpp0_i32<0x118>(v);
     v += dpp_i32<0x142, 0xA>(0, v);
     v += dpp_i32<0x143, 0xC>(0, v);
     return v;
