@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define PTV_API_VERSION 6
+#define PTV_API_VERSION 7
 
 /* error codes */
 #define PTV_OK 0
@@ -221,6 +221,30 @@ typedef struct {
     double mad_eps;
 } ptv_filter_params;
 
+/*
+ * Linear interpolation over a Delaunay triangulation: method='linear', the reference's default
+ * (interpolator.py:196-197 `griddata(points, values, grid_coords, method='linear',
+ * fill_value=0.0)` -> scipy LinearNDInterpolator).  The caller builds
+ * `tri = scipy.spatial.Delaunay(points)` on the host, exactly as LinearNDInterpolator does (Qhull),
+ * and passes its arrays; the GPU locates every voxel in it (walk from a simplex incident to the
+ * voxel's nearest particle, scipy's brute-force scan where the walk meets a degenerate simplex)
+ * and interpolates with scipy's barycentric arithmetic.  Arrays follow numpy's C layouts
+ * (int32 / float64) and live in the call's memory space.
+ */
+typedef struct {
+    int64_t nsimplex;
+    const int32_t *simplices;         /* (nsimplex, 4) particle indices: tri.simplices */
+    const int32_t *neighbors;         /* (nsimplex, 4) tri.neighbors (-1 = hull face) */
+    const double *transform;          /* (nsimplex, 4, 3) tri.transform (NaN rows: degenerate) */
+    const int32_t *vertex_to_simplex; /* (n,) a simplex incident to each particle (walk start;
+                                         tri.vertex_to_simplex with tri.coplanar points filled in) */
+    double min_bound[3], max_bound[3];/* tri.min_bound, tri.max_bound */
+    double fill_value;                /* griddata fill_value (0.0 in interpolator.py:197) */
+    const uint8_t *fluid_mask;        /* as ptv_knn_params.fluid_mask */
+    uint32_t flags;                   /* PTV_FLAG_NAN_TO_NUM only */
+    int chunk_planes;                 /* z planes per nearest-particle + walk chunk (multiple of 4), <= 0: auto */
+} ptv_linear_params;
+
 /* Library / device management. */
 int ptv_version(void);
 /* sizeof(ptv_particles, ptv_grid, ptv_knn_params, ptv_stats, ptv_rbf_params, ptv_div_params):
@@ -228,6 +252,8 @@ int ptv_version(void);
 int ptv_abi_sizes(int64_t out6[6]);
 /* sizeof(ptv_mask_grid, ptv_boundary_params, ptv_filter_params): the same self-check */
 int ptv_abi_sizes2(int64_t out3[3]);
+/* sizeof(ptv_linear_params): the same self-check */
+int ptv_abi_sizes3(int64_t out1[1]);
 const char *ptv_last_error(void);
 int ptv_device_count(int *out);
 int ptv_init(int device, ptv_ctx **out);
@@ -273,6 +299,23 @@ int ptv_interp_rbf_local(ptv_ctx *ctx, const ptv_particles *p, const ptv_grid *g
 int ptv_interp_rbf_local_dev(ptv_ctx *ctx, const ptv_particles *p, const ptv_grid *g,
                              const ptv_rbf_params *prm, double *U, double *V, double *W,
                              void *stream, ptv_stats *st);
+
+/*
+ * Linear (Delaunay) interpolation, host buffers.  Replaces the griddata branch for
+ * method='linear' (interpolator.py:196-197): LinearNDInterpolator's point location
+ * (_find_simplex: bounding-box test, directed walk, brute force) and barycentric
+ * interpolation (interpnd _do_evaluate), fill_value outside the hull.  Outputs as
+ * ptv_interp_knn (float64).
+ */
+int ptv_interp_linear(ptv_ctx *ctx, const ptv_particles *p, const ptv_grid *g,
+                      const ptv_linear_params *prm, double *U, double *V, double *W,
+                      ptv_stats *st);
+
+/* Same on device pointers (particles, grid, triangulation arrays, mask, outputs); enqueued on
+ * `stream`, synchronises once at the end (the brute-force count decides a second kernel). */
+int ptv_interp_linear_dev(ptv_ctx *ctx, const ptv_particles *p, const ptv_grid *g,
+                          const ptv_linear_params *prm, double *U, double *V, double *W,
+                          void *stream, ptv_stats *st);
 
 /*
  * Consistent divergence, host buffers: H2D of the fields and mask, one stencil kernel,

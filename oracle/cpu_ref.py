@@ -413,6 +413,52 @@ def interp_grid_parallel(points, values, ax, ay, az, method="idw", k=8, power=2.
     return U, V, W
 
 
+# ---------------------------------------------------------------------------
+# method='linear': griddata(points, values, xi, method='linear', fill_value=0.0)
+# (interpolator.py:196-197) = scipy LinearNDInterpolator: Delaunay (Qhull) + point location
+# (spatial/_qhull.pyx _find_simplex) + barycentric interpolation (interpolate/interpnd.pyx
+# _do_evaluate).  scipy 1.15.3 (the reference container's) is a third-party dependency; its
+# published algorithm restated: Delaunay.find_simplex runs the same walk from the same start
+# sequence (eps = 100 DBL_EPSILON), then
+#   c_i = ((0 + T_i0 (x_0 - r_0)) + T_i1 (x_1 - r_1)) + T_i2 (x_2 - r_2), c_3 = ((1 - c_0) - c_1) - c_2
+#   out = (((0 + c_0 v_s0) + c_1 v_s1) + c_2 v_s2) + c_3 v_s3,  fill_value where no simplex.
+# Pinned bit-exactly by tests/golden/linear_*.npz (the reference interpolate_field itself).
+# ---------------------------------------------------------------------------
+def linear_points(points, values, queries, fill_value=0.0, tri=None):
+    from scipy.spatial import Delaunay
+
+    points = np.ascontiguousarray(points, dtype=np.float64)
+    values = np.asarray(values, dtype=np.float64)
+    q = np.ascontiguousarray(queries, dtype=np.float64).reshape(-1, 3)
+    tri = Delaunay(points) if tri is None else tri
+    s = tri.find_simplex(q)
+    ok = s >= 0
+    T = tri.transform[np.where(ok, s, 0)]
+    d = q - T[:, 3, :]
+    c = []
+    for i in range(3):
+        ci = np.zeros(len(q))
+        for j in range(3):
+            ci = ci + T[:, i, j] * d[:, j]
+        c.append(ci)
+    c.append(((1.0 - c[0]) - c[1]) - c[2])
+    vv = values[tri.simplices[np.where(ok, s, 0)]]  # (m, 4, 3)
+    out = np.zeros((len(q), values.shape[1]))
+    for j in range(4):
+        out = out + c[j][:, None] * vv[:, j]
+    out[~ok] = fill_value
+    return out
+
+
+def linear_grid(points, values, ax, ay, az, fill_value=0.0, z0=0, z1=None):
+    """(U, V, W) each (nz', ny, nx) of griddata(method='linear') on the separable grid."""
+    q = grid_queries(ax, ay, az, z0, z1)
+    z1 = len(az) if z1 is None else z1
+    out = linear_points(points, values, q, fill_value)
+    shp = (z1 - z0, len(ay), len(ax))
+    return tuple(out[:, c].reshape(shp) for c in range(3))
+
+
 def lattice_axis(a, step=4):
     """The library's coarse-lattice axis (ptv_api.cpp prepare / k_subsample): every `step`-th
     value of `a` plus the last."""

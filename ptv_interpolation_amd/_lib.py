@@ -13,7 +13,8 @@ import threading
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("PTV_LIB", os.path.join(HERE, "libptv_amd.so"))
+_DEFAULT_LIB = os.path.join(HERE, "libptv_amd.so")
+LIB_PATH = os.environ.get("PTV_LIB", _DEFAULT_LIB)
 
 PTV_OK = 0
 PTV_E_ARG = -1
@@ -69,6 +70,16 @@ class RbfParams(C.Structure):
                 ("flags", C.c_uint32), ("chunk_planes", C.c_int)]
 
 
+_i32p = C.POINTER(C.c_int32)
+
+
+class LinearParams(C.Structure):
+    _fields_ = [("nsimplex", C.c_int64), ("simplices", _i32p), ("neighbors", _i32p), ("transform", _dp),
+                ("vertex_to_simplex", _i32p), ("min_bound", C.c_double * 3), ("max_bound", C.c_double * 3),
+                ("fill_value", C.c_double), ("fluid_mask", C.POINTER(C.c_uint8)), ("flags", C.c_uint32),
+                ("chunk_planes", C.c_int)]
+
+
 F64 = 0
 F32 = 1
 FLAG_OUT_F32 = 2  # U, V, W written as float32 (main.py:230 astype, fused)
@@ -121,6 +132,11 @@ EXPORTS = {
     "ptv_version": (C.c_int, []),
     "ptv_abi_sizes": (C.c_int, [C.POINTER(C.c_int64)]),
     "ptv_abi_sizes2": (C.c_int, [C.POINTER(C.c_int64)]),
+    "ptv_abi_sizes3": (C.c_int, [C.POINTER(C.c_int64)]),
+    "ptv_interp_linear": (C.c_int, [C.c_void_p, C.POINTER(Particles), C.POINTER(Grid), C.POINTER(LinearParams),
+                                    _dp, _dp, _dp, C.POINTER(Stats)]),
+    "ptv_interp_linear_dev": (C.c_int, [C.c_void_p, C.POINTER(Particles), C.POINTER(Grid),
+                                        C.POINTER(LinearParams), _dp, _dp, _dp, C.c_void_p, C.POINTER(Stats)]),
     "ptv_last_error": (C.c_char_p, []),
     "ptv_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "ptv_init": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
@@ -173,6 +189,8 @@ def lib():
                     "(hipcc, gfx950). The k-NN path has no CPU fallback.")
             L = C.CDLL(LIB_PATH)
             for name, (res, args) in EXPORTS.items():
+                if LIB_PATH != _DEFAULT_LIB and not hasattr(L, name):
+                    continue  # an older build under PTV_LIB (same-box A/B): its missing entry points stay unbound
                 fn = getattr(L, name)
                 fn.restype = res
                 fn.argtypes = args
@@ -226,6 +244,39 @@ def abi_sizes2():
     out = (C.c_int64 * 3)()
     check(lib().ptv_abi_sizes2(out))
     return list(out), [C.sizeof(MaskGrid), C.sizeof(BoundaryParams), C.sizeof(FilterParams)]
+
+
+def abi_sizes3():
+    """(C sizeof, ctypes sizeof) of ptv_linear_params."""
+    out = (C.c_int64 * 1)()
+    check(lib().ptv_abi_sizes3(out))
+    return list(out), [C.sizeof(LinearParams)]
+
+
+class Triangulation:
+    """The arrays of ``scipy.spatial.Delaunay(points)`` the linear kernels read, as contiguous
+    int32 / float64 (``tri.transform`` is scipy's own barycentric transforms, computed on first
+    access exactly as LinearNDInterpolator does).  Particles that are not vertices (Qhull
+    "coplanar" points, e.g. duplicates) start their walks in the simplex Qhull assigned them."""
+
+    def __init__(self, tri):
+        self.simplices = np.ascontiguousarray(tri.simplices, dtype=np.int32)
+        self.neighbors = np.ascontiguousarray(tri.neighbors, dtype=np.int32)
+        self.transform = np.ascontiguousarray(tri.transform, dtype=np.float64)
+        v2s = np.array(tri.vertex_to_simplex, dtype=np.int32)
+        cp = np.asarray(tri.coplanar)
+        if cp.size:
+            v2s[cp[:, 0]] = cp[:, 1]
+        self.vertex_to_simplex = np.ascontiguousarray(v2s)
+        self.min_bound = [float(v) for v in tri.min_bound]
+        self.max_bound = [float(v) for v in tri.max_bound]
+        self.nsimplex = int(self.simplices.shape[0])
+
+    def params(self, fill_value=0.0, fluid_mask=None, flags=0, chunk_planes=0):
+        return LinearParams(self.nsimplex, self.simplices.ctypes.data_as(_i32p), self.neighbors.ctypes.data_as(_i32p),
+                            as_dp(self.transform), self.vertex_to_simplex.ctypes.data_as(_i32p),
+                            (C.c_double * 3)(*self.min_bound), (C.c_double * 3)(*self.max_bound), float(fill_value),
+                            fluid_mask, int(flags), int(chunk_planes))
 
 
 def device_count() -> int:
@@ -503,6 +554,69 @@ class Context:
                                          as_dp(out[0]), as_dp(out[1]), as_dp(out[2]), C.byref(st)))
         self.stats = st.as_dict()
         return tuple(out)
+
+    def interp_linear(self, points, values, tri, axes=None, grid_points=None, shape=None, fill_value=0.0,
+                      fluid_mask=None, flags=0, z_range=None, chunk_planes=0, out=None):
+        """Host-array linear (Delaunay) interpolation (griddata(method='linear') semantics) over
+        ``tri`` (a Triangulation of these points).  Returns (U, V, W) float64 (nz', ny, nx)."""
+        pts = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 3)
+        vals = np.ascontiguousarray(values, dtype=np.float64).reshape(-1, 3)
+        cols = [np.ascontiguousarray(pts[:, i]) for i in range(3)] + [np.ascontiguousarray(vals[:, i]) for i in range(3)]
+        P = Particles(pts.shape[0], *[as_dp(c) for c in cols])
+        keep = list(cols)
+        if axes is not None:
+            ax, ay, az = (np.ascontiguousarray(a, dtype=np.float64).ravel() for a in axes)
+            nx, ny, nz = len(ax), len(ay), len(az)
+            keep += [ax, ay, az]
+            G = Grid(nx, ny, nz, as_dp(ax), as_dp(ay), as_dp(az), None, None, None, 0, nz)
+        else:
+            gp = [np.ascontiguousarray(a, dtype=np.float64).ravel() for a in grid_points]
+            ft = _flat_tiles(gp, shape, fluid_mask, z_range)
+            if ft is not None:
+                gp, tshape, fm, unpad = ft
+                res = self.interp_linear(points, values, tri, grid_points=gp, shape=tshape, fill_value=fill_value,
+                                         fluid_mask=fm, flags=flags, chunk_planes=chunk_planes)
+                return tuple(unpad(a) for a in res)
+            nz, ny, nx = shape
+            keep += gp
+            G = Grid(nx, ny, nz, None, None, None, as_dp(gp[0]), as_dp(gp[1]), as_dp(gp[2]), 0, nz)
+        z0, z1 = (0, nz) if z_range is None else z_range
+        G.z_begin, G.z_end = z0, z1
+        mk = None
+        if fluid_mask is not None:
+            mk = np.ascontiguousarray(fluid_mask, dtype=np.uint8).reshape(nz, ny, nx)
+            keep.append(mk)
+        prm = tri.params(fill_value, mk.ctypes.data_as(C.POINTER(C.c_uint8)) if mk is not None else None, flags,
+                         chunk_planes)
+        out = _outputs(out, (z1 - z0, ny, nx), np.float64)
+        st = Stats()
+        check(lib().ptv_interp_linear(self.h, C.byref(P), C.byref(G), C.byref(prm),
+                                      as_dp(out[0]), as_dp(out[1]), as_dp(out[2]), C.byref(st)))
+        self.stats = st.as_dict()
+        return tuple(out)
+
+    def interp_linear_dev(self, n, pptrs, nx, ny, nz, tri_ptrs, nsimplex, min_bound, max_bound, axes_ptrs=None,
+                          point_ptrs=None, out_ptrs=None, fill_value=0.0, mask_ptr=0, flags=0, z_range=None,
+                          stream=0, chunk_planes=0):
+        """Device-pointer linear interpolation; tri_ptrs: device (simplices, neighbors, transform,
+        vertex_to_simplex).  Returns the call's stats."""
+        P = Particles(int(n), *[dev_dp(p) for p in pptrs])
+        if axes_ptrs is not None:
+            G = Grid(nx, ny, nz, *[dev_dp(p) for p in axes_ptrs], None, None, None, 0, nz)
+        else:
+            G = Grid(nx, ny, nz, None, None, None, *[dev_dp(p) for p in point_ptrs], 0, nz)
+        z0, z1 = (0, nz) if z_range is None else z_range
+        G.z_begin, G.z_end = z0, z1
+        i32 = lambda p: C.cast(C.c_void_p(p), _i32p)
+        prm = LinearParams(int(nsimplex), i32(tri_ptrs[0]), i32(tri_ptrs[1]), dev_dp(tri_ptrs[2]), i32(tri_ptrs[3]),
+                           (C.c_double * 3)(*min_bound), (C.c_double * 3)(*max_bound), float(fill_value),
+                           C.cast(C.c_void_p(mask_ptr), C.POINTER(C.c_uint8)) if mask_ptr else None, int(flags),
+                           int(chunk_planes))
+        st = Stats()
+        check(lib().ptv_interp_linear_dev(self.h, C.byref(P), C.byref(G), C.byref(prm),
+                                          *[dev_dp(p) for p in out_ptrs], C.c_void_p(stream) if stream else None,
+                                          C.byref(st)))
+        return st.as_dict()
 
     def interp_rbf_dev(self, n, pptrs, nx, ny, nz, axes_ptrs=None, point_ptrs=None, out_ptrs=None, k=20,
                        kernel="thin_plate_spline", epsilon=1.0, degree=1, smoothing=0.0, smoothing_ptr=0,

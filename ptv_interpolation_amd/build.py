@@ -19,7 +19,7 @@ CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 LIB = os.path.join(HERE, "libptv_amd.so")
 BUILD = os.path.join(HERE, "csrc", "_build")
-SOURCES = ["ptv_api.cpp", "ptv_bin.hip", "ptv_knn.hip", "ptv_rbf.hip", "ptv_div.hip", "ptv_mask.hip", "ptv_filter.hip"]
+SOURCES = ["ptv_api.cpp", "ptv_bin.hip", "ptv_knn.hip", "ptv_rbf.hip", "ptv_div.hip", "ptv_mask.hip", "ptv_filter.hip", "ptv_linear.hip"]
 ARCH = os.environ.get("PTV_OFFLOAD_ARCH", "gfx950")
 # per-file extras: the local-RBF kernel keeps each voxel's system row in registers, so every
 # loop over the row must unroll fully (a partial unroll turns the row into scratch memory)

@@ -91,6 +91,9 @@ struct ptv_ctx {
     bool div_pending = false;
     std::vector<hipEvent_t> rbf_ev;                              // 3 per chunk: knn start, solve start, end
     int rbf_chunks = 0;
+    DevBuf<int> lin_simp, lin_nbr, lin_v2s, lin_count;           // linear: triangulation (host calls), flags
+    DevBuf<double> lin_tr;
+    DevBuf<long long> lin_flags;                                 // linear: voxels left to the brute force
     double *h_bbox = nullptr;  // pinned, 6 doubles
     unsigned long long *h_misc = nullptr;  // pinned scratch words (cull count, halo bound)
     ptv_stats last{};
@@ -128,6 +131,15 @@ int ptv_abi_sizes2(int64_t out3[3]) {
     out3[0] = (int64_t)sizeof(ptv_mask_grid);
     out3[1] = (int64_t)sizeof(ptv_boundary_params);
     out3[2] = (int64_t)sizeof(ptv_filter_params);
+    return PTV_OK;
+}
+
+int ptv_abi_sizes3(int64_t out1[1]) {
+    if (!out1) {
+        set_error("ptv_abi_sizes3: out is NULL");
+        return PTV_E_ARG;
+    }
+    out1[0] = (int64_t)sizeof(ptv_linear_params);
     return PTV_OK;
 }
 
@@ -204,6 +216,12 @@ int ptv_free(ptv_ctx *c) {
     c->slots.release();
     c->rbf_pw.release();
     c->rbf_status.release();
+    c->lin_simp.release();
+    c->lin_nbr.release();
+    c->lin_v2s.release();
+    c->lin_count.release();
+    c->lin_tr.release();
+    c->lin_flags.release();
     c->smooth.release();
     for (auto &b : c->fld) b.release();
     c->mask_axes.release();
@@ -800,6 +818,91 @@ int run_rbf(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_rbf
     return PTV_OK;
 }
 
+// method='linear' on device pointers: binning + k = 1 slot search per z-chunk (the walk starts),
+// the walk / interpolation kernel, then scipy's brute-force location for the flagged voxels.
+constexpr int kLinearMaxWalk = 4096;
+constexpr int kLinearFlagCap = 1 << 20;
+
+int run_linear(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_linear_params *prm,
+               const int32_t *simp, const int32_t *nbr, const double *tr, const int32_t *v2s, const double *ax,
+               const double *ay, const double *az, const double *qx, const double *qy, const double *qz,
+               const uint8_t *mask, double *U, double *V, double *W, hipStream_t s) {
+    const SearchParams sp{PTV_METHOD_NEAREST, 1, 2.0, 1e-10, 0u, 0.0, 0.0, 0};
+    KnnLaunch kl;
+    Binned b{};
+    PTV_TRY(prepare(c, p, g, &sp, ax, ay, az, qx, qy, qz, s, kl, b));
+    const int64_t plane = g->nx * g->ny;
+    const int64_t z0 = g->z_begin, z1 = g->z_end;
+    int cp = prm->chunk_planes;
+    if (cp <= 0) cp = (int)std::max<int64_t>(4, std::min<int64_t>(z1 - z0, ((int64_t)512 << 20) / std::max<int64_t>(plane * 4, 1)));
+    cp = std::max(4, (cp + 3) & ~3);
+    PTV_TRY(c->slots.ensure((size_t)std::min<int64_t>(cp, z1 - z0) * plane));
+    PTV_TRY(c->lin_count.ensure(1));
+    PTV_TRY(c->lin_flags.ensure(kLinearFlagCap));
+    PTV_HIP(hipMemsetAsync(c->lin_count.p, 0, sizeof(int), s));
+    const int nchunks = (int)((z1 - z0 + cp - 1) / cp);
+    while ((int)c->rbf_ev.size() < 3 * nchunks) {
+        hipEvent_t e;
+        PTV_HIP(hipEventCreate(&e));
+        c->rbf_ev.push_back(e);
+    }
+    LinearKernelArgs la{};
+    la.nx = (int)g->nx;
+    la.ny = (int)g->ny;
+    la.out_z0 = (int)z0;
+    la.separable = ax != nullptr ? 1 : 0;
+    la.nsimplex = prm->nsimplex;
+    la.simplices = simp;
+    la.neighbors = nbr;
+    la.transform = tr;
+    la.v2s = v2s;
+    la.pu = p->u;
+    la.pv = p->v;
+    la.pw = p->w;
+    for (int d = 0; d < 3; ++d) {
+        la.lo[d] = prm->min_bound[d];
+        la.hi[d] = prm->max_bound[d];
+    }
+    la.fill = prm->fill_value;
+    la.flags = prm->flags;
+    la.max_walk = kLinearMaxWalk;
+    la.flag_count = c->lin_count.p;
+    la.flag_list = c->lin_flags.p;
+    la.flag_cap = kLinearFlagCap;
+    for (int ch = 0; ch < nchunks; ++ch) {
+        const int za = (int)(z0 + (int64_t)ch * cp), zb = (int)std::min<int64_t>(z1, za + cp);
+        KnnLaunch cl = kl;
+        cl.z0 = za;
+        cl.z1 = zb;
+        cl.lz0 = (int)z0;
+        cl.mode = kModeSlots;
+        cl.slots = c->slots.p;
+        PTV_HIP(hipEventRecord(c->rbf_ev[3 * ch], s));
+        PTV_TRY(launch_knn(cl, b, ax, ay, az, qx, qy, qz, mask, nullptr, nullptr, nullptr, s));
+        PTV_HIP(hipEventRecord(c->rbf_ev[3 * ch + 1], s));
+        la.z0 = za;
+        la.z1 = zb;
+        PTV_TRY(launch_linear(la, b.prec, c->slots.p, ax, ay, az, qx, qy, qz, mask, U, V, W, s));
+        PTV_HIP(hipEventRecord(c->rbf_ev[3 * ch + 2], s));
+    }
+    c->rbf_chunks = nchunks;
+    int nflag = 0;
+    PTV_HIP(hipMemcpyAsync(&nflag, c->lin_count.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    PTV_HIP(hipStreamSynchronize(s));
+    if (nflag > kLinearFlagCap) {
+        set_error("linear: " + std::to_string(nflag) + " voxels need the brute-force point location (limit " +
+                  std::to_string(kLinearFlagCap) + "): degenerate triangulation");
+        return PTV_E_UNSUPPORTED;
+    }
+    c->last.n_singular = nflag;  // reported: voxels located by the brute-force scan
+    if (nflag > 0) {
+        la.z0 = (int)z0;
+        la.z1 = (int)z1;
+        PTV_TRY(launch_linear_brute(la, nflag, ax, ay, az, qx, qy, qz, U, V, W, s));
+    }
+    return PTV_OK;
+}
+
 int finish_timing(ptv_ctx *c) {
     float ms = 0.f;
     if (c->div_pending) {
@@ -1049,6 +1152,66 @@ int ptv_interp_rbf_local(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, 
                           int64_t nsing = 0;
                           const int rc = run_rbf(c, dp, dg, prm, m, dg->ax, dg->ay, dg->az, dg->px, dg->py, dg->pz,
                                                  dsmooth, dmask, dU, dV, dW, s, &nsing);
+                          c->timed_pending = true;
+                          return rc;
+                      }));
+    if (st) *st = c->last;
+    return PTV_OK;
+}
+
+static int validate_linear(const ptv_particles *p, const ptv_linear_params *prm) {
+    if (!prm || !prm->simplices || !prm->neighbors || !prm->transform || !prm->vertex_to_simplex) {
+        set_error("linear: NULL parameters or triangulation array");
+        return PTV_E_ARG;
+    }
+    if (prm->nsimplex < 1 || prm->nsimplex > 0x7fffffffLL) {
+        set_error("linear: nsimplex must be in [1, 2^31)");
+        return PTV_E_ARG;
+    }
+    if (p->n > 0x7fffffffLL) {
+        set_error("linear: more than 2^31 particles");
+        return PTV_E_ARG;
+    }
+    if (prm->flags & ~PTV_FLAG_NAN_TO_NUM) {
+        set_error("linear: only PTV_FLAG_NAN_TO_NUM is supported");
+        return PTV_E_UNSUPPORTED;
+    }
+    return PTV_OK;
+}
+
+int ptv_interp_linear_dev(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_linear_params *prm,
+                          double *U, double *V, double *W, void *stream, ptv_stats *st) {
+    PTV_TRY(check_call(c, p, g, prm, U, V, W));
+    PTV_TRY(validate_linear(p, prm));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    const bool sep = g->ax && g->ay && g->az;
+    const int rc = run_linear(c, p, g, prm, prm->simplices, prm->neighbors, prm->transform, prm->vertex_to_simplex,
+                              sep ? g->ax : nullptr, sep ? g->ay : nullptr, sep ? g->az : nullptr,
+                              sep ? nullptr : g->px, sep ? nullptr : g->py, sep ? nullptr : g->pz, prm->fluid_mask, U,
+                              V, W, s);
+    c->timed_pending = true;
+    if (st) *st = c->last;
+    return rc;
+}
+
+int ptv_interp_linear(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_linear_params *prm,
+                      double *U, double *V, double *W, ptv_stats *st) {
+    PTV_TRY(check_call(c, p, g, prm, U, V, W));
+    PTV_TRY(validate_linear(p, prm));
+    PTV_TRY(host_call(c, p, g, prm->fluid_mask, nullptr, U, V, W,
+                      [&](const ptv_particles *dp, const ptv_grid *dg, const uint8_t *dmask, const double *,
+                          double *dU, double *dV, double *dW, hipStream_t s) {
+                          const size_t ns = (size_t)prm->nsimplex, n = (size_t)p->n;
+                          PTV_TRY(c->lin_simp.ensure(4 * ns));
+                          PTV_TRY(c->lin_nbr.ensure(4 * ns));
+                          PTV_TRY(c->lin_tr.ensure(12 * ns));
+                          PTV_TRY(c->lin_v2s.ensure(n));
+                          PTV_HIP(hipMemcpyAsync(c->lin_simp.p, prm->simplices, 4 * ns * sizeof(int), hipMemcpyHostToDevice, s));
+                          PTV_HIP(hipMemcpyAsync(c->lin_nbr.p, prm->neighbors, 4 * ns * sizeof(int), hipMemcpyHostToDevice, s));
+                          PTV_HIP(hipMemcpyAsync(c->lin_tr.p, prm->transform, 12 * ns * sizeof(double), hipMemcpyHostToDevice, s));
+                          PTV_HIP(hipMemcpyAsync(c->lin_v2s.p, prm->vertex_to_simplex, n * sizeof(int), hipMemcpyHostToDevice, s));
+                          const int rc = run_linear(c, dp, dg, prm, c->lin_simp.p, c->lin_nbr.p, c->lin_tr.p, c->lin_v2s.p,
+                                                    dg->ax, dg->ay, dg->az, dg->px, dg->py, dg->pz, dmask, dU, dV, dW, s);
                           c->timed_pending = true;
                           return rc;
                       }));

@@ -124,6 +124,36 @@ struct DivArgs {
 int launch_divergence(const DivArgs &a, const void *U, const void *V, const void *W, const uint8_t *M, void *out,
                       hipStream_t s);
 
+// ---- linear (ptv_linear.hip): griddata(method='linear') over scipy's Delaunay triangulation ----
+struct LinearKernelArgs {
+    int nx, ny;          // grid plane
+    int z0, z1;          // planes of this launch (chunk)
+    int out_z0;          // plane of output row 0 (the slab start)
+    int separable;
+    long long nsimplex;
+    const int *simplices;     // (nsimplex, 4) particle indices
+    const int *neighbors;     // (nsimplex, 4) neighbour opposite vertex k, -1 = hull
+    const double *transform;  // (nsimplex, 4, 3) barycentric transforms (NaN: degenerate)
+    const int *v2s;           // (n,) a simplex incident to each particle (start of the walk)
+    const double *pu, *pv, *pw;  // values, original particle order
+    double lo[3], hi[3];      // Delaunay min_bound / max_bound
+    double fill;              // fill_value
+    uint32_t flags;           // PTV_FLAG_NAN_TO_NUM
+    int max_walk;             // walk steps before the brute-force fallback
+    int *flag_count;          // voxels left to the brute force (device counter)
+    long long *flag_list;     // their slab-relative voxel indices
+    int flag_cap;
+};
+
+// slots: (z1 - z0, ny, nx) nearest-particle slots (launch_knn kModeSlots, k = 1)
+int launch_linear(const LinearKernelArgs &a, const double4 *prec, const uint32_t *slots, const double *ax,
+                  const double *ay, const double *az, const double *qx, const double *qy, const double *qz,
+                  const uint8_t *mask, double *U, double *V, double *W, hipStream_t s);
+// scipy's brute-force point location for the nflag voxels the walk flagged (after every chunk)
+int launch_linear_brute(const LinearKernelArgs &a, int nflag, const double *ax, const double *ay, const double *az,
+                        const double *qx, const double *qy, const double *qz, double *U, double *V, double *W,
+                        hipStream_t s);
+
 // ---- local RBF (ptv_rbf.hip) ----
 constexpr int kRbfMaxSystem = 64;  // k + #monomials per voxel system
 

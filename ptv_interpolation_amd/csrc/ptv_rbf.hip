@@ -726,7 +726,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     // rows x 8R entries): 80 KB per block at R = 2, two blocks (the register budget's 2 waves
     // per SIMD) per CU
     constexpr int SC = 4 * (16 * R) * (8 * R) > 4 * 32 * 4 + 4 * 32 / 2 ? 4 * (16 * R) * (8 * R) : 4 * 32 * 4 + 4 * 32 / 2;
-    __shared__ double s_sc[4][SC];
+    __shared__ double s_sc[4][SC];  // (80 KB per block with s_ye: two blocks per CU, not a byte more)
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int seg = lane >> 4, li = lane & 15;
     double4 *ye = s_ye[wid][seg];
@@ -797,8 +797,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     rbf_wave_sync();  // the values' LDS is the build scratch next
 
     // ---- 2. symmetric build of rows li and li + 16: row i evaluates phi for the columns
-    //      (i + d) mod NR, d = 1..H, into its segment's scratch (column swizzled by the row:
-    //      conflict-free stores); entry (i, j) is then its own (d = (j - i) mod NR <= H) or its
+    //      (i + d) mod NR, d = 1..H, into a row-swizzled slot of its segment's scratch
+    //      (conflict-free stores); entry (i, j) is then its own (d = (j - i) mod NR <= H) or its
     //      partner row j's (d' = NR - d).  H phi per row instead of k. ----
     constexpr int NR = 16 * R, H = NR / 2;
     double *ss = sc + seg * (NR * H);
@@ -819,18 +819,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         }
     }
     rbf_wave_sync();  // the partner rows' entries are read next
+    double dg[R];  // the diagonal: phi(0) + smoothing, 1 on padded rows (identity block)
+#pragma unroll
+    for (int q = 0; q < R; ++q) dg[q] = li + 16 * q < k ? diag : 1.0;
     double A[R][M];
 #pragma unroll
     for (int j = 0; j < M; ++j) {
 #pragma unroll
         for (int q = 0; q < R; ++q) {
             const int row = li + 16 * q;
+            // branch-free addresses: own slot (dj in 1..H) or the partner row j's (dj in H+1..NR-1);
+            // dj = 0 (the diagonal) reads a stale slot of the row and takes dg instead.
+            // Padded rows and columns hold 0 (the build writes e = 0 there).
             const int dj = (j - row) & (NR - 1);
-            const int addr = dj == 0 ? 0
-                             : (dj <= H ? row * H + ((dj - 1) ^ (row & (H - 1)))
-                                        : j * H + ((NR - dj - 1) ^ (j & (H - 1))));
-            const double e = ss[addr];
-            A[q][j] = (row >= k || j >= k) ? (j == row ? 1.0 : 0.0) : (dj == 0 ? diag : e);
+            const int own = row * H + (((dj - 1) & (H - 1)) ^ (row & (H - 1)));
+            const int par = j * H + ((NR - 1 - dj) ^ (j & (H - 1)));
+            const double e = ss[dj <= H ? own : par];
+            A[q][j] = dj == 0 ? dg[q] : e;
         }
         if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // bounded reads in flight
     }

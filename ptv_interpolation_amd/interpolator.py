@@ -12,15 +12,17 @@ root ``interpolator.py`` re-exports this module):
     sample_mask_on_grid  interpolator.py:205-238
     extract_boundary_particles  interpolator.py:240-284
 
-``interpolate_field(method='idw'|'sibson'|'nearest'|'rbf')`` runs the k-NN search
+``interpolate_field(method='idw'|'sibson'|'nearest'|'rbf'|'linear')`` runs the k-NN search
 and the weighted average (or the local RBF solve) as HIP kernels through the C ABI
 (include/ptv_api.h).  There is no CPU fallback for these methods: a missing library
 or GPU raises.  Results reproduce the reference arithmetic (see
 ptv_interpolation_amd/csrc/ptv_knn.hip); ``n_jobs`` is accepted and ignored by the
 GPU methods (the reference uses it only for RBF, interpolator.py:173).  ``nearest``
 is a scipy ``griddata`` call in the reference (interpolator.py:196-197), i.e. a k = 1
-KDTree query, and runs on the same k-NN kernel here; ``linear``/``cubic`` (Qhull
-Delaunay) stay scipy ``griddata`` calls (outside the accelerated path).
+KDTree query, and runs on the same k-NN kernel here.  ``linear`` (the reference default,
+griddata -> LinearNDInterpolator) triangulates with the same scipy Delaunay (Qhull) call on
+the host and locates / interpolates every voxel on the GPU (ptv_linear.hip).  ``cubic``
+stays a scipy ``griddata`` call (it raises for 3-D data, as in the reference).
 """
 from __future__ import annotations
 
@@ -276,8 +278,37 @@ def interpolate_field(df, grid_tuple, method="linear", rbf_neighbors=20, rbf_ker
         # griddata(method='nearest') (interpolator.py:196-197) is NearestNDInterpolator: the
         # k = 1 query of the same GPU k-NN kernel, values of the nearest particle
         return _knn_field(points, values, grid_tuple, "nearest", 1, 2.0)
-    # 'linear' / 'cubic' griddata (Qhull Delaunay): not part of the accelerated path
+    if method == "linear":
+        return _linear_field(points, values, grid_tuple)
+    # 'cubic' (and anything else) goes to griddata as in the reference, which raises for 3-D data
     from scipy.interpolate import griddata
 
     out = griddata(points, values, (X, Y, Z), method=method, fill_value=0.0)
     return out[..., 0], out[..., 1], out[..., 2]
+
+
+def _linear_field(points, values, grid_tuple, fill_value=0.0):
+    """griddata(points, values, (X, Y, Z), method='linear', fill_value=0.0) (interpolator.py:197).
+
+    The triangulation is ``scipy.spatial.Delaunay(points)`` -- the same Qhull call
+    LinearNDInterpolator makes, so the simplices and barycentric transforms are the reference's
+    own (and Qhull's errors for degenerate inputs are raised unchanged); every voxel's point
+    location and barycentric interpolation run on the GPU (ptv_linear.hip), z-slabs over the
+    devices like the k-NN methods."""
+    from scipy.spatial import Delaunay
+
+    X, Y, Z = np.broadcast_arrays(*grid_tuple)
+    shape = np.shape(X)
+    tri = _lib.Triangulation(Delaunay(np.ascontiguousarray(points, dtype=np.float64)))
+    axes = separable_axes(X, Y, Z)
+    if axes is not None:
+        full = [np.empty((len(axes[2]), len(axes[1]), len(axes[0]))) for _ in range(3)]
+        U, V, W = launcher.run_slabs(len(axes[2]), lambda ctx, z0, z1, views: ctx.interp_linear(
+            points, values, tri, axes=axes, fill_value=fill_value, z_range=(z0, z1), out=views), full)
+    else:
+        ctx = _lib.Context.get(launcher.devices()[0])
+        size = int(np.prod(shape))
+        g = [np.ascontiguousarray(np.asarray(A, dtype=np.float64)).reshape(-1) for A in (X, Y, Z)]
+        sh = tuple(shape) if len(shape) == 3 else (1, 1, size)
+        U, V, W = ctx.interp_linear(points, values, tri, grid_points=g, shape=sh, fill_value=fill_value)
+    return U.reshape(shape), V.reshape(shape), W.reshape(shape)

@@ -43,6 +43,8 @@ def test_struct_layouts_agree():
     assert c == py
     c2, py2 = _lib.abi_sizes2()
     assert c2 == py2
+    c3, py3 = _lib.abi_sizes3()
+    assert c3 == py3
 
 
 def test_no_gpu_fails_loudly():

@@ -259,3 +259,29 @@ def test_c3_full_size_gaussian_sampled(ctx):
         e_ref, e_exact, gap = normwise(got, lap[:, c]), normwise(got, ext[:, c]), normwise(lap[:, c], ext[:, c])
         print(f"C3 {'UVW'[c]}: gpu-vs-lapack {e_ref:.3e}  gpu-vs-exact {e_exact:.3e}  lapack-vs-exact {gap:.3e}")
         assert e_exact <= max(TOL, TRUTH_FACTOR * gap)
+
+
+def test_spd_register_kernel_rerun_matches_lds_kernel(ctx, monkeypatch):
+    """SPD systems (gaussian, degree -1) run k_rbf_spd16 (v_rcp_f64 + Newton reciprocals only);
+    a pivot outside that range (here: scalar smoothing 2e307 puts every diagonal pivot above
+    2^1020) makes the host rerun the launch with k_rbf_spd, which adds the IEEE division for such
+    pivots.  Both kernels eliminate in the same order with the same reciprocals wherever the
+    fast one serves; their evaluation sums differ in order (16-lane rows of two entries vs a
+    32-lane segment sum), so on these ill-conditioned systems they agree to TOL_ILL (checked on
+    a normal case with PTV_RBF_SPD=1 forcing the LDS kernel), and the rerun matches the oracle."""
+    from oracle import cpu_ref
+    from ptv_interpolation_amd.rbf import LocalRBFInterpolator
+
+    P, Q, ax = _rand_case(63, 4000, 12)
+    fast = LocalRBFInterpolator(P, Q, neighbors=32, kernel="gaussian", epsilon=0.3, degree=-1).evaluate_grid(ax, ax, ax)
+    monkeypatch.setenv("PTV_RBF_SPD", "1")
+    lds = LocalRBFInterpolator(P, Q, neighbors=32, kernel="gaussian", epsilon=0.3, degree=-1).evaluate_grid(ax, ax, ax)
+    monkeypatch.delenv("PTV_RBF_SPD")
+    for a, b in zip(fast, lds):
+        assert normwise(a, b) <= TOL_ILL
+    big = LocalRBFInterpolator(P, Q, neighbors=32, kernel="gaussian", epsilon=0.3, degree=-1,
+                               smoothing=2e307).evaluate_grid(ax, ax, ax)
+    ref = cpu_ref.rbf_local_grid(P, Q, ax, ax, ax, 32, kernel="gaussian", epsilon=0.3, degree=-1, smoothing=2e307)
+    for a, b in zip(big, ref):
+        assert np.isfinite(a).all()
+        assert normwise(a, b) <= TOL

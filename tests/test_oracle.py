@@ -175,3 +175,15 @@ def test_idw_radius_oracle_matches_bruteforce():
                 continue
             w = 1.0 / (np.sqrt(d2[sel]) ** p + 1e-10)
             np.testing.assert_allclose(got[i], (w[:, None] * Q[sel]).sum(0) / w.sum(), rtol=1e-13, atol=1e-15)
+
+
+@pytest.mark.parametrize("name", names(("linear_",)))
+def test_linear_oracle_matches_reference(name):
+    """method='linear' restatement (Delaunay.find_simplex + interpnd arithmetic) against the
+    reference interpolate_field fixtures, bit for bit."""
+    from oracle import cpu_ref
+
+    g = load(name)
+    out = cpu_ref.linear_grid(g["points"], g["values"], g["ax"], g["ay"], g["az"])
+    for a, c in zip(out, "UVW"):
+        assert np.array_equal(a, g[c])
