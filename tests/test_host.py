@@ -62,11 +62,17 @@ def test_reference_exceptions_before_any_gpu_call(capsys):
 
 
 def test_griddata_methods_pass_through():
-    """linear stays scipy griddata (interpolator.py:196-197, Qhull: outside the accelerated path);
-    nearest runs on the GPU k-NN kernel (tests/test_gpu_nearest_div.py)."""
+    """'cubic' stays scipy griddata (interpolator.py:196-197), which rejects 3-D data exactly as
+    in the reference; 'linear' runs on the GPU (tests/test_gpu_linear.py) and, with no GPU
+    visible, fails loudly instead of falling back to the CPU."""
     grid, _ = ip.create_grid(((0, 4),) * 3, 4)
-    U, V, W = ip.interpolate_field(_df(60), grid, method="linear")
-    assert U.shape == (4, 4, 4) and np.isfinite(U).all()
+    with pytest.raises(ValueError, match="cubic"):
+        ip.interpolate_field(_df(60), grid, method="cubic")
+    from ptv_interpolation_amd import _lib
+
+    if _lib.device_count() == 0:
+        with pytest.raises((ValueError, _lib.PtvError)):
+            ip.interpolate_field(_df(60), grid, method="linear")
 
 
 def test_load_ptv_data_renames(tmp_path):
