@@ -61,6 +61,7 @@ METRIC_C5 = ("Mvoxels/s interpolated + achieved HBM GB/s, 2048³ grid / 50M part
              "(z-slab partition)")
 METRIC_DIV = "Mvoxels/s + achieved HBM GB/s, consistent divergence (physics.py:6-53) of a 512³ field"
 METRIC_FILTER = "Mparticles/s filtered + achieved HBM GB/s, k-NN median/MAD outlier filter (filtering.py:5-58), 5M particles"
+METRIC_LINEAR = "Mvoxels/s interpolated + achieved HBM GB/s, griddata(method='linear') over a Delaunay triangulation"
 METRIC_MASK = ("Mvoxels/s + achieved HBM GB/s, pore-mask path (sample_mask_on_grid + extract_boundary_particles, "
                "interpolator.py:205-284), 512³ mask")
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -116,7 +117,8 @@ def parse():
     ap.add_argument("--power", type=float, default=2.0)
     ap.add_argument("--radius", type=float, default=None,
                     help="idw: fixed-radius search (PTV_METHOD_IDW_RADIUS, an extension) instead of k-NN")
-    ap.add_argument("--method", default=None, choices=["idw", "sibson", "nearest", "rbf", "div", "filter", "mask"])
+    ap.add_argument("--method", default=None,
+                    choices=["idw", "sibson", "nearest", "rbf", "linear", "div", "filter", "mask"])
     ap.add_argument("--div-dtype", default="f64", choices=["f64", "f32"],
                     help="--method div: field dtype (f32 = the C5 fp32 field, Python-float spacings)")
     ap.add_argument("--rbf-kernel", default=None, help="rbf: scipy kernel name (default thin_plate_spline)")
@@ -885,8 +887,97 @@ def main_mask(args):
         dist.destroy_process_group()
 
 
+def main_linear(args):
+    """--method linear: one step = griddata(method='linear') (interpolator.py:196-197, the reference
+    default) on resident data: binning + the k = 1 slot search (walk starts) + the point-location walk
+    and barycentric interpolation of every voxel (ptv_linear.hip).  The triangulation is built once on
+    the host by scipy's Delaunay (Qhull, as LinearNDInterpolator does) before the timed region; its
+    wall time is reported next to the step (`host_triangulation_s`).  Defaults 256^3 / 1M particles
+    (--config c2 size).  Weak scaling: each rank interpolates its own copy."""
+    import torch
+    from scipy.spatial import Delaunay
+
+    world, rank, local, dist, dev = _dist_init()
+    from ptv_interpolation_amd import _lib, synth
+
+    G = args.grid if args.config != "headline" or args.grid != 512 else 256
+    n = args.particles if args.config != "headline" or args.particles != 5_000_000 else 1_000_000
+    P, _ = synth.sphere_pack(n, G)
+    Q = np.random.default_rng(20261017 + rank).standard_normal((n, 3))
+    t0 = time.perf_counter()
+    d = Delaunay(P)
+    tri = _lib.Triangulation(d)  # includes scipy's transform (LinearNDInterpolator computes it too)
+    t_host = time.perf_counter() - t0
+    ax_h = np.linspace(0, G - 1, G)
+    cols = [torch.from_numpy(np.ascontiguousarray(P[:, i])).to(dev) for i in range(3)] + \
+           [torch.from_numpy(np.ascontiguousarray(Q[:, i])).to(dev) for i in range(3)]
+    axes = [torch.from_numpy(ax_h.copy()).to(dev) for _ in range(3)]
+    tarr = [torch.from_numpy(a).to(dev) for a in (tri.simplices, tri.neighbors, tri.transform, tri.vertex_to_simplex)]
+    out = [torch.empty((G, G, G), dtype=torch.float64, device=dev) for _ in range(3)]
+    ctx = _lib.Context(local)
+    torch.cuda.set_stream(torch.cuda.Stream(dev))
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        return ctx.interp_linear_dev(n, [c.data_ptr() for c in cols], G, G, G, [t.data_ptr() for t in tarr],
+                                     tri.nsimplex, tri.min_bound, tri.max_bound,
+                                     axes_ptrs=[a.data_ptr() for a in axes], out_ptrs=[o.data_ptr() for o in out],
+                                     stream=stream)
+
+    elapsed, w_ms = _timed(step, args, dist, dev, "ms_solve", ctx)
+    st = ctx.last_stats()
+    wavg = float(np.mean(w_ms))
+    V = G ** 3
+    inside = float((out[0] != 0).double().mean().item())
+    # per voxel inside the hull: the containing simplex's transform (96 B) and vertex ids (16 B), the
+    # 4 vertices' values (4 x 24 B); every voxel: its walk-start slot (4 B) + the 3 outputs (24 B)
+    alg = int(V * inside) * (96 + 16 + 96) + V * (4 + 24)
+    ach = alg / (wavg * 1e-3) / 1e9
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            from scipy.interpolate import LinearNDInterpolator
+
+            ip = LinearNDInterpolator(d, Q, fill_value=0.0)  # reuses the triangulation and its transform
+            nz_s = max(1, min(G, 2_000_000 // (G * G)))
+            Z, Y, X = np.meshgrid(ax_h[G // 2 - nz_s // 2:G // 2 - nz_s // 2 + nz_s], ax_h, ax_h, indexing="ij")
+            t = time.perf_counter()
+            ip((X, Y, Z))
+            dt = time.perf_counter() - t
+            cpu = {"value": round(X.size / dt / 1e6, 4), "unit": "Mvoxels/s", "cores": 1, "kind": "port",
+                   "cpu_model": cpu_model(),
+                   "sample": f"{nz_s} central z-planes ({X.size} voxels) of the same workload: scipy "
+                             "LinearNDInterpolator evaluation over the same prebuilt Delaunay (the reference's "
+                             "griddata minus its Qhull build), 1 process", "seconds": round(dt, 2)}
+        except Exception as e:
+            cpu = {"value": None, "error": repr(e)[:200]}
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC_LINEAR, "value": round(V * world / (elapsed / args.steps) / 1e6, 2),
+            "unit": "Mvoxels/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic: generate_sphere_pack.py geometry scaled to voxel units, N(0,1) velocities",
+            "config": {"workload": f"griddata(method='linear') {G}^3 grid / {n} particles ({tri.nsimplex} simplices, "
+                                   f"{inside:.1%} of voxels inside the hull)", "grid": G, "particles": n,
+                       "method": "linear", "parallelism": f"independent copies x{world}"},
+            "host_triangulation_s": round(t_host, 2),
+            "breakdown_ms": {"bin": round(st["ms_bin"], 3), "lattice": round(st["ms_lattice"], 3),
+                             "nearest_slots": round(st["ms_knn"], 3), "walk": round(wavg, 3)},
+            "brute_force_voxels": int(st["n_singular"]),
+            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None, "kernel": "k_linear_walk",
+                         "alg_bytes_per_launch": alg, "kernel_ms": round(wavg, 4)},
+            "cpu_baseline": cpu}), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.method == "linear":
+        return main_linear(args)
     if args.method == "div":
         return main_div(args)
     if args.method == "filter":

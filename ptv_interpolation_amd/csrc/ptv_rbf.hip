@@ -81,6 +81,50 @@ __device__ __forceinline__ void rbf_wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// exp(x) for x <= 0, bit-identical to the device libm (ocml) exp this kernel used before: the
+// same reduction (x log2 e rounded to even, Cody-Waite ln 2 in two parts), degree-11 polynomial
+// in Horner form, ldexp and underflow to 0 below -1075.  Written out so that every Horner step is
+// one VOP3 v_fma_f64 with its coefficient in an SGPR pair: the compiler's form kept the
+// coefficients in VGPRs and paid a v_mov_b64 per step (v_fmac overwrites its addend).
+__device__ __forceinline__ double horner(double r, double p, double c) {
+    double o;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(o) : "v"(r), "v"(p), "s"(c));
+    return o;
+}
+__device__ __forceinline__ double exp_nonpos(double x) {
+    const double dn = __builtin_rint(x * 0x1.71547652b82fep+0);
+    double r = fma(-0x1.62e42fefa39efp-1, dn, x);
+    r = fma(-0x1.abc9e3b39803fp-56, dn, r);
+    double p = fma(0x1.ade156a5dcb37p-26, r, 0x1.28af3fca7ab0cp-22);
+    p = horner(r, p, 0x1.71dee623fde64p-19);
+    p = horner(r, p, 0x1.a01997c89e6b0p-16);
+    p = horner(r, p, 0x1.a01a014761f6ep-13);
+    p = horner(r, p, 0x1.6c16c1852b7b0p-10);
+    p = horner(r, p, 0x1.1111111122322p-7);
+    p = horner(r, p, 0x1.55555555502a1p-5);
+    p = horner(r, p, 0x1.5555555555511p-3);
+    p = horner(r, p, 0x1.000000000000bp-1);
+    p = fma(r, p, 1.0);
+    p = fma(r, p, 1.0);
+    const double e = __builtin_amdgcn_ldexp(p, (int)dn);
+    return -1075.0 > x ? 0.0 : e;
+}
+
+// IEEE sqrt for x >= 2^-767 (the LLVM gfx9 f64 expansion without its small-input rescale),
+// branch-free; +-0 and +inf are returned as they are.  For 0 < x < 2^-767 it may differ from
+// sqrt() in the last bit, which no SPD kernel can see: phi(r) of the gaussian, inverse
+// multiquadric and inverse quadratic kernels only uses r * r + 1 or exp(-r * r).
+__device__ __forceinline__ double sqrt_spd(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = y * 0.5;
+    const double r = fma(-h, g, 0.5);
+    g = fma(g, r, g);
+    h = fma(h, r, h);
+    g = fma(fma(-g, g, x), h, g);
+    g = fma(fma(-g, g, x), h, g);
+    return __builtin_amdgcn_class(x, 0x260) ? x : g;  // +inf, +0, -0
+}
+
 // scipy/interpolate/_rbfinterp_pythran.py kernel functions (r >= 0)
 template <int KERN>
 __device__ __forceinline__ double rbf_phi(double r) {
@@ -91,7 +135,7 @@ __device__ __forceinline__ double rbf_phi(double r) {
     if constexpr (KERN == PTV_RBF_MULTIQUADRIC) return -sqrt(r * r + 1.0);
     if constexpr (KERN == PTV_RBF_INVERSE_MULTIQUADRIC) return 1.0 / sqrt(r * r + 1.0);
     if constexpr (KERN == PTV_RBF_INVERSE_QUADRATIC) return 1.0 / (r * r + 1.0);
-    if constexpr (KERN == PTV_RBF_GAUSSIAN) return exp(-(r * r));
+    if constexpr (KERN == PTV_RBF_GAUSSIAN) return exp_nonpos(-(r * r));
     return 0.0;
 }
 
@@ -813,7 +857,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
             if (row < k && j < k) {
                 const double4 yj = ye[j];
                 const double dx = yi[q].x - yj.x, dy = yi[q].y - yj.y, dz = yi[q].z - yj.z;
-                e = rbf_phi<KERN>(sqrt((dx * dx + dy * dy) + dz * dz));
+                e = rbf_phi<KERN>(sqrt_spd((dx * dx + dy * dy) + dz * dz));
             }
             ss[row * H + ((dd - 1) ^ (row & (H - 1)))] = e;
         }
@@ -864,15 +908,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     for (int c = 0; c < M; ++c) {
         const int pq = c / 16;
         // c is a constant in the unrolled loop, so the row_newbcast lane folds to one
-        singular = singular || piv == 0.0;
-        const double ap = fabs(piv);
-        slow = slow | ((ap <= 0x1p-1020) & (piv != 0.0)) | !(ap < 0x1p1020);  // bitwise: no branches
+        singular = singular | (piv == 0.0);
         rd[pq] = li == (c & 15) ? rp : rd[pq];
+        // multipliers: a row set wholly below the pivot needs no test, a finished one none at all
+        // (a zero pivot leaves garbage multipliers: the call then fails with PTV_E_SINGULAR)
         double l[R];
 #pragma unroll
         for (int q = 0; q < R; ++q) {
             const int row = li + 16 * q;
-            l[q] = (16 * q + 15 > c && row > c && row < M && piv != 0.0) ? A[q][c] * rp : 0.0;
+            if (16 * q + 15 <= c) l[q] = 0.0;
+            else if (16 * q > c) l[q] = A[q][c] * rp;
+            else l[q] = row > c ? A[q][c] * rp : 0.0;
         }
         double pivn = 0.0, rpn = 1.0;
 #pragma unroll
@@ -897,6 +943,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         rp = rpn;
         __builtin_amdgcn_sched_barrier(0);  // keep the steps apart (register pressure)
     }
+
+    // a pivot outside the Newton reciprocal's range shows in the reciprocals this lane kept
+    // (huge pivot: |1/p| tiny or 0; tiny or subnormal: overflow; NaN: NaN)
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        const double ar = fabs(rd[q]);
+        slow = slow | !(ar >= 0x1p-1020 && ar <= 0x1p1020);
+    }
+    slow = slow & !singular;
 
     // ---- 4. back substitution: x_c = b_c * (1 / U_cc) from lane c % 16.  Row r's b no longer
     //      changes after step r (only rows above c are updated), so every lane scales its own
