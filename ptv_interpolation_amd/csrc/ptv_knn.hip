@@ -251,19 +251,27 @@ __device__ __forceinline__ void insert(double (&bd)[KMAX], int (&bp)[KMAX], doub
     // first j where it holds, slot j takes the carry (the candidate, then each displaced
     // entry) and hands its old entry on.  Ties keep the earlier entry first.  Every slot is
     // updated in place (selects on v_cmp masks, no exec-mask branches).
+    // On a sorted list the carry is never below bd[j] once it differs from d2, so the distance
+    // slot is min(bd[j], carry) and the new carry the max (one op each).  One asm block per slot
+    // updates bd[j] and bp[j] IN PLACE (the carries go to fresh registers): written with
+    // separate selects, the compiler renamed the list every step and paid 14 moves per insert
+    // at the loop back-edge to put it back.
     double cd = d2;
     int cp = p;
 #pragma unroll
     for (int j = 0; j < KMAX; ++j) {
-        // on a sorted list the carry is never below bd[j] once it differs from d2, so the
-        // distance slot is min(bd[j], carry) and the new carry the max (one op each)
-        const bool mj = d2 < bd[j];
-        const double od = bd[j];
-        const int op = bp[j];
-        bd[j] = vmin_f64(od, cd);
-        cd = vmax_f64(od, cd);
-        bp[j] = mj ? cp : op;
-        cp = mj ? op : cp;
+        double ncd;
+        int ncp;
+        asm("v_cmp_lt_f64 vcc, %[d2], %[bd]\n\t"
+            "v_max_f64 %[nc], %[bd], %[cd]\n\t"
+            "v_min_f64 %[bd], %[bd], %[cd]\n\t"
+            "v_cndmask_b32 %[np], %[cp], %[bp], vcc\n\t"
+            "v_cndmask_b32 %[bp], %[bp], %[cp], vcc"
+            : [bd] "+v"(bd[j]), [bp] "+v"(bp[j]), [nc] "=&v"(ncd), [np] "=&v"(ncp)
+            : [d2] "v"(d2), [cd] "v"(cd), [cp] "v"(cp)
+            : "vcc");
+        cd = ncd;
+        cp = ncp;
     }
 }
 
