@@ -523,7 +523,11 @@ def main_interp(args):
         flops = (zb - za) * G * G * rbf_flops_per_voxel(k, m_sys)
         tf = flops / (avg["ms_solve"] * 1e-3) / 1e12
         roof = {"bound": "fp64", "achieved": round(tf, 2), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(tf / FP64_PEAK_TFLOPS, 4), "traffic": None, "kernel": f"k_rbf_local<{(m_sys + 7) & ~7}>",
+                "frac": round(tf / FP64_PEAK_TFLOPS, 4), "traffic": None,
+                # the launcher's choice (ptv_rbf.hip rbf_spd): SPD kernels without a polynomial, M <= 32
+                "kernel": (f"k_rbf_spd16<{(m_sys + 7) & ~7}>"
+                           if args.rbf_kernel in ("gaussian", "inverse_multiquadric", "inverse_quadratic")
+                           and m_sys == k and (m_sys + 7) & ~7 <= 32 else f"k_rbf_local<{(m_sys + 7) & ~7}>"),
                 "alg_flops_per_launch": flops, "kernel_ms": round(avg["ms_solve"], 3),
                 "knn_slots_ms": round(avg["ms_knn"], 3)}
     else:

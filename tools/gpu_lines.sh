@@ -1,0 +1,29 @@
+#!/bin/bash
+# Every bench line of the round in one GPU call (config lines + the rows next to the path), each
+# under its own time limit; stops at the first failure.  Output: gpurun_out/<tag>_lines/<name>.json
+# usage: gpurun -- bash tools/gpu_lines.sh r02
+set -o pipefail
+tag=${1:-r02}
+cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
+out=gpurun_out/${tag}_lines
+mkdir -p "$out"
+run() {  # name, time limit, bench args...
+  local name=$1 lim=$2; shift 2
+  echo "== $name: bench.py $*"
+  timeout -k 10 "$lim" python -u bench.py "$@" > "$out/$name.json" 2> "$out/$name.err" || { echo "FAILED $name"; tail -5 "$out/$name.err"; exit 1; }
+  tail -c 400 "$out/$name.json"; echo
+}
+run headline 300
+run nearest 300 --method nearest --no-e2e
+run sibson 300 --method sibson --k 30 --no-e2e --no-cpu-baseline
+run idw_k50 400 --method idw --k 50 --steps 5 --warmup 1 --no-e2e --no-cpu-baseline
+run c2 300 --config c2
+run c2r 300 --config c2r
+run c3 600 --config c3
+run c4 600 --config c4 --steps 5 --warmup 1
+run c5 900 --config c5 --steps 3 --warmup 1 --no-cpu-baseline
+run linear 600 --method linear --steps 10 --warmup 2
+run filter 300 --method filter
+run mask 300 --method mask
+run div_f64 300 --method div
+run div_f32 300 --method div --div-dtype f32
