@@ -260,6 +260,15 @@ __device__ __forceinline__ void insert(double (&bd)[KMAX], int (&bp)[KMAX], doub
     int cp = p;
 #pragma unroll
     for (int j = 0; j < KMAX; ++j) {
+        if (j == KMAX - 1) {  // the last slot: no carry leaves the list
+            asm("v_cmp_lt_f64 vcc, %[d2], %[bd]\n\t"
+                "v_min_f64 %[bd], %[bd], %[cd]\n\t"
+                "v_cndmask_b32 %[bp], %[bp], %[cp], vcc"
+                : [bd] "+v"(bd[j]), [bp] "+v"(bp[j])
+                : [d2] "v"(d2), [cd] "v"(cd), [cp] "v"(cp)
+                : "vcc");
+            break;
+        }
         double ncd;
         int ncp;
         asm("v_cmp_lt_f64 vcc, %[d2], %[bd]\n\t"
@@ -398,8 +407,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
     }
 
     // upper bound on this voxel's k-th distance from the coarse lattice (triangle inequality)
-    double ub = INFINITY;
-    if (a.cb.dk != nullptr && active) {
+    auto lattice_ub = [&]() -> double {
+        double u = INFINITY;
+        if (a.cb.dk == nullptr || !active) return u;
         // |v - c| in fp32 from lattice-relative offsets, rounded up: any upper bound is valid
         // the tile is one lattice cell: its corners are wave-uniform (scalar loads)
         const int j0[3] = {__builtin_amdgcn_readfirstlane(cx >> kLatticeShift),
@@ -413,10 +423,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
             const float ex = (float)(qx - a.cb.ax[jx]), ey = (float)(qy - a.cb.ay[jy]), ez = (float)(qz - a.cb.az[jz]);
             const float e2 = __fmaf_rn(ez, ez, __fmaf_rn(ey, ey, ex * ex));
             const double D = a.cb.dk[((size_t)jz * a.cb.n[1] + jy) * a.cb.n[0] + jx];
-            ub = fmin(ub, D + (double)(sqrtf_up(e2) * 1.000002f));
+            u = fmin(u, D + (double)(sqrtf_up(e2) * 1.000002f));
         }
-        ub = ub * (1.0 + 1e-9) + a.cg.mg;
-    }
+        return u * (1.0 + 1e-9) + a.cg.mg;
+    };
+    // With seed records the seeds' bound is the tighter one for (nearly) every lane: the
+    // D(c) + |v - c| bound is then formed only when some active lane got no seed bound.
+    bool seeds_defer = false;
+    if constexpr (KMAX <= 8) seeds_defer = a.cb.recs != nullptr;
+    double ub = seeds_defer ? INFINITY : lattice_ub();
     // candidates at or beyond the bound can never be among the k nearest
     double ub2 = !active ? -1.0 : (ub < INFINITY ? ub * ub : INFINITY);
     // radius mode: every candidate with d2 <= R^2 counts (the list stays unused)
@@ -533,6 +548,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
                     if (st2 < ub2) {
                         ub2 = st2;
                         ub = sqrt_up(st2);
+                    }
+                }
+                if (__builtin_amdgcn_ballot_w64(active && !(kth < INFINITY)) != 0) {
+                    // rare (fewer than k distinct seeds survived the hash): the lattice bound
+                    const double u = lattice_ub();
+                    if (u < ub) {
+                        ub = u;
+                        ub2 = u * u;
                     }
                 }
                 seeded = true;
