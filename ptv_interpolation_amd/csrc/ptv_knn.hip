@@ -366,7 +366,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ?
     const int rr = b / a.ntxb;
     const int ty = rr % a.nty;
     const int tz = rr / a.nty;
-    const int tx = bx * 4 + wid;
+    const int tx = __builtin_amdgcn_readfirstlane(bx * 4 + wid);  // wave-uniform: scalar tile-box loads
     if (tx >= a.ntx) return;  // wave-uniform
     const int ix = tx * 4 + (lane & 3);
     const int iy = ty * 4 + ((lane >> 2) & 3);
