@@ -141,9 +141,11 @@ def test_spherepack_voids_vs_oracle(ctx, k):
     assert np.array_equal(U, Ur) and np.array_equal(V, Vr) and np.array_equal(W, Wr)
 
 
-@pytest.mark.parametrize("G,N,k", [(256, 1_000_000, 8), (512, 5_000_000, 8)])
+@pytest.mark.parametrize("G,N,k", [(256, 1_000_000, 8), (512, 5_000_000, 8), (256, 1_000_000, 50),
+                                   (512, 5_000_000, 50)])
 def test_full_size_sampled(ctx, G, N, k):
-    """Headline sizes: every voxel computed on the GPU, 20k random voxels checked bit-exact vs KDTree."""
+    """Headline sizes, k = 8 and the reference default k = 50 (interpolator.py:65): every voxel
+    computed on the GPU, 20k random voxels checked bit-exact vs KDTree."""
     from oracle import cpu_ref
     from ptv_interpolation_amd import synth
 
