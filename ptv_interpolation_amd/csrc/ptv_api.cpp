@@ -558,6 +558,8 @@ int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchP
         ll.cb.az = lat[l + 1].az;
         ll.cb.dk = lat[l + 1].dk;
         ll.cb.recs = lat[l + 1].recs;
+        if (const char *e = std::getenv("PTV_LAT_SEEDS"))  // dev knob: 0 = lattice levels unseeded
+            if (e[0] == '0') ll.cb.recs = nullptr;
         for (int d = 0; d < 3; ++d) ll.cb.n[d] = lat[l + 1].n[d];
         PTV_TRY(launch_knn(ll, b, lat[l].ax, lat[l].ay, lat[l].az, nullptr, nullptr, nullptr, nullptr, lat[l].dk,
                            lat[l].dk, lat[l].dk, s));
