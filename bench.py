@@ -33,7 +33,8 @@ interpolator.py:126-155 (scipy KDTree + numpy) over z-slabs on a ProcessPoolExec
 interpolator.py:173-182 / test_parallel.py pattern — on a bounded sample of the same workload,
 with the CPU model and the calibration against the reference (profiles/cpu_calibration_*.json).
 ``--method div|filter|mask`` bench the rows next to the path (physics.py / filtering.py /
-the pore-mask path) with their own metric lines.
+the pore-mask path) with their own metric lines; ``--method linear`` benches griddata(method=
+'linear') (the reference default) with the host Delaunay build timed apart from the GPU step.
 """
 from __future__ import annotations
 
