@@ -52,7 +52,10 @@ namespace ptv {
 #define PTV_KNN_WAVES 4  // waves per SIMD the k <= 8 kernels are register-capped for
 #endif
 #ifndef PTV_KNN_WAVES_BIG
-#define PTV_KNN_WAVES_BIG 1  // k > 8: no cap (the split modes reach 2 waves per SIMD up to KMAX = 32)
+#define PTV_KNN_WAVES_BIG 1  // k > 32: no cap
+#endif
+#ifndef PTV_KNN_WAVES_MID
+#define PTV_KNN_WAVES_MID 3  // 8 < KMAX <= 32: capped for 3 waves per SIMD (Sibson k=30 and the RBF k=32 slot search -7 %)
 #endif
 
 constexpr int kStampFields = 8;
@@ -326,7 +329,8 @@ __device__ __forceinline__ double axis_gap(int c, double o, double cs, double lo
 // modes carry no interpolation epilogue: one kernel for every mode put the KMAX = 32 lists at
 // 284 registers (one wave per SIMD); split, every KMAX <= 32 kernel runs two waves per SIMD.
 template <int KMAX, bool STAMP, int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KMAX <= 8 ? PTV_KNN_WAVES : PTV_KNN_WAVES_BIG))) void k_knn_interp(KnnKernelArgs a, const double4 *__restrict__ prec,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
+    KMAX <= 8 ? PTV_KNN_WAVES : (KMAX <= 32 ? PTV_KNN_WAVES_MID : PTV_KNN_WAVES_BIG)))) void k_knn_interp(KnnKernelArgs a, const double4 *__restrict__ prec,
                                                     const double4 *__restrict__ pval,
                                                     const uint32_t *__restrict__ cstart,
                                                     const double *__restrict__ ax, const double *__restrict__ ay,
