@@ -52,7 +52,7 @@ namespace ptv {
 #define PTV_KNN_WAVES 4  // waves per SIMD the k <= 8 kernels are register-capped for
 #endif
 #ifndef PTV_KNN_WAVES_BIG
-#define PTV_KNN_WAVES_BIG 1  // k > 32: no cap
+#define PTV_KNN_WAVES_BIG 2  // KMAX > 32: capped for 2 waves per SIMD (spills, yet k = 50 -30 %: one wave could not hide its latency)
 #endif
 #ifndef PTV_KNN_WAVES_MID
 #define PTV_KNN_WAVES_MID 3  // 8 < KMAX <= 32: capped for 3 waves per SIMD (Sibson k=30 and the RBF k=32 slot search -7 %)
