@@ -54,6 +54,9 @@ namespace ptv {
 #ifndef PTV_KNN_WAVES_BIG
 #define PTV_KNN_WAVES_BIG 2  // KMAX > 32: capped for 2 waves per SIMD (spills, yet k = 50 -30 %: one wave could not hide its latency)
 #endif
+#ifndef PTV_KNN_WAVES_SMALL
+#define PTV_KNN_WAVES_SMALL 5  // KMAX = 4 (nearest, radius, k <= 4): 5 waves per SIMD (nearest -2 %)
+#endif
 #ifndef PTV_KNN_WAVES_MID
 #define PTV_KNN_WAVES_MID 3  // 8 < KMAX <= 32: capped for 3 waves per SIMD (Sibson k=30 and the RBF k=32 slot search -7 %)
 #endif
@@ -330,7 +333,7 @@ __device__ __forceinline__ double axis_gap(int c, double o, double cs, double lo
 // 284 registers (one wave per SIMD); split, every KMAX <= 32 kernel runs two waves per SIMD.
 template <int KMAX, bool STAMP, int MODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
-    KMAX <= 8 ? PTV_KNN_WAVES : (KMAX <= 32 ? PTV_KNN_WAVES_MID : PTV_KNN_WAVES_BIG)))) void k_knn_interp(KnnKernelArgs a, const double4 *__restrict__ prec,
+    KMAX <= 4 ? PTV_KNN_WAVES_SMALL : (KMAX <= 8 ? PTV_KNN_WAVES : (KMAX <= 32 ? PTV_KNN_WAVES_MID : PTV_KNN_WAVES_BIG))))) void k_knn_interp(KnnKernelArgs a, const double4 *__restrict__ prec,
                                                     const double4 *__restrict__ pval,
                                                     const uint32_t *__restrict__ cstart,
                                                     const double *__restrict__ ax, const double *__restrict__ ay,
