@@ -7,23 +7,36 @@ resident in HBM: bounding box + particle binning + coarse-lattice bounds + the k
 writing U, V, W (the reference rebuilds its KDTree on every call, interpolator.py:132, so the
 binning is inside the step).
 
-    python bench.py [--gpus N --steps K --warmup W] [--config headline|c2|c3|c4|c5]
+    python bench.py [--gpus N --steps K --warmup W] [--config headline|c2|c3|c4|c5|...]
     torchrun --nproc-per-node N bench.py --gpus N ...          (one process per GPU, RCCL)
+
+``--gpus N`` with N > 1 and no torchrun environment starts the N ranks itself: the parent
+process, which has not touched a GPU, runs ``python -m torch.distributed.run --nproc-per-node
+N bench.py ...`` as a child and exits with its code; each rank checks that the world size it
+was given equals ``--gpus`` and fails loudly otherwise.
 
 Multi-GPU = the north_star partition (zslab.py): ONE grid cut into z-slabs,
 rank r computing planes slab_bounds(nz, N)[r], the particle set replicated in every rank's HBM
-(all-gather / broadcast before the timed loop) and culled on device to the slab's window with
-a proof of exactness (ptv_knn_params.slab_halo; a failed proof widens the halo, never changes
-a result).  No collective touches the timed step; an RCCL all-gather reassembly of the full
-field is timed once after it and reported apart (``allgather_ms``).
+(broadcast before the timed loop) and culled on device to the slab's window with a proof of
+exactness (ptv_knn_params.slab_halo; a failed proof widens the halo, never changes a result).
+No collective touches the timed step; an RCCL all-gather reassembly of the full field (slabs
+padded to the largest one when they differ) is timed once after it and reported apart
+(``allgather_ms``).
 
-* headline: weak scaling.  The grid is 512 x 512 x 512N: N stacked sphere-pack copies along z
-  (5M particles each, all 5M N replicated on every rank), rank r owns copy r's 512^3 planes.
+* headline (default): strong scaling of the named 512^3 / 5M workload: every N computes the
+  same grid, rank r its 512/N planes.
+* headline_weak: N stacked 512^3 sphere-pack copies along z (5M particles each, all 5M N
+  replicated on every rank), rank r owns copy r's 512^3 planes.
 * c2 (256^3 / 1M IDW), c3 (512^3 / 5M local Gaussian RBF 32 x 32), c4 (1024^3 / 10M IDW with
   the sphere-pack pore mask fused), c5 (2048^3 / 50M IDW, float32 field, + the consistent
   divergence of view_divergence.py over each slab with a one-plane halo interpolated
   redundantly): strong scaling of the named grid, the configs' N = 1 line being the whole grid
   on one GPU.
+
+``--share R/N`` (one GPU, no collective) runs rank R's step of the N-rank strong partition:
+the per-rank step time a rehearsal of the N-GPU run is built from (tools/gpu_scaling.sh).
+``--dry-run`` (CPU, gloo) runs the launcher and the partition / broadcast / padded all-gather
+with a plane-index fill in place of the kernel (tests/test_bench_launch.py).
 
 Rank 0 prints ONE JSON line.  ``roofline.achieved`` = algorithmic bytes of the k-NN kernel
 (SURVEY.md §8(d) gather model, V (6k 8 + 3 s_out) for this rank's slab) / its hipEvent-timed
@@ -71,7 +84,8 @@ KMAX_LIST = (4, 8, 12, 16, 24, 32, 40, 48, 56, 64)  # k_knn_interp instantiation
 
 # BASELINE.json configs; C1 (64^3 / 10k, CPU plumbing) is a parity test case
 CONFIGS = {
-    "headline": dict(grid=512, particles=5_000_000, method="idw", k=8, scaling="weak", metric=METRIC),
+    "headline": dict(grid=512, particles=5_000_000, method="idw", k=8, scaling="strong", metric=METRIC),
+    "headline_weak": dict(grid=512, particles=5_000_000, method="idw", k=8, scaling="weak", metric=METRIC),
     "c2": dict(grid=256, particles=1_000_000, method="idw", k=8, scaling="strong", metric=METRIC_C2),
     # BASELINE config 2 as named ("IDW radius-search"): an extension, the reference has no radius
     # search (parity unpinned; tests/test_gpu_radius.py); r = 3 voxels ~ 6.8 particles per ball
@@ -108,7 +122,12 @@ def rbf_flops_per_voxel(k, m):
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="number of GPUs (ranks); > 1 without torchrun's env starts the ranks itself")
+    ap.add_argument("--share", default=None, metavar="R/N",
+                    help="one GPU: time rank R's step of the N-rank strong z-slab partition (rehearsal)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU/gloo: launcher + partition + padded all-gather, a plane-index fill for the kernel")
     ap.add_argument("--steps", type=int, default=None, help="timed steps (default 20; 5 for c3, c5)")
     ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 5; 2 for c3, c5)")
     ap.add_argument("--config", default="headline", choices=sorted(CONFIGS))
@@ -306,11 +325,25 @@ def cpu_baseline_rbf(args, P, Q, ax):
                      f"building its own tree (interpolator.py:173-182 pattern)", dt)
 
 
-def _dist_init():
+def env_world():
+    """(world, rank, local rank) from torchrun's environment (1, 0, 0 without one)."""
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def check_world(args, world):
+    """--gpus must name the world size the ranks were started with (fail loudly, never run
+    a different N than the one the line would report)."""
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the world size is {world} "
+                         f"(start N ranks with torchrun --nproc-per-node N, or --gpus N alone)")
+
+
+def _dist_init(args=None):
     """One process per GPU (torchrun env); returns (world, rank, local, dist or None, device)."""
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = env_world()
+    if args is not None:
+        check_world(args, world)
     import torch
 
     torch.cuda.set_device(local)
@@ -320,7 +353,50 @@ def _dist_init():
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if dist.get_world_size() != world:
+            raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks, expected {world}")
     return world, rank, local, dist, torch.device("cuda", local)
+
+
+def launch_ranks(n):
+    """Start n ranks of this script under torch.distributed.run (a child process: this process
+    has not initialised the GPU and is not replaced) and return their exit code."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+def allgather_padded(slab, counts, dist):
+    """Reassemble the full (sum(counts), ...) field on every rank from the ranks' (counts[r], ...)
+    slabs: one all_gather_into_tensor of slabs padded to max(counts) planes, then the padding
+    dropped (zslab.gather_field; uneven slabs when N does not divide nz)."""
+    from ptv_interpolation_amd import zslab
+
+    return zslab.gather_field(slab, dist, counts=counts)
+
+
+@contextlib.contextmanager
+def pinned_device(device):
+    """PTV_DEVICE=device for the drop-in calls inside the block, the previous value restored."""
+    old = os.environ.get("PTV_DEVICE")
+    os.environ["PTV_DEVICE"] = str(device)
+    try:
+        yield
+    finally:
+        if old is None:
+            os.environ.pop("PTV_DEVICE", None)
+        else:
+            os.environ["PTV_DEVICE"] = old
 
 
 def _timed(step, args, dist, dev, stat_key, ctx):
@@ -368,10 +444,29 @@ def _device_fluid_mask(G, nz_grid, planes, dev):
     return m
 
 
+def parse_share(share):
+    """'R/N' -> (R, N) with 0 <= R < N."""
+    try:
+        r, n = (int(v) for v in share.split("/"))
+    except ValueError:
+        raise SystemExit(f"bench.py: --share wants R/N, got {share!r}")
+    if not (n >= 1 and 0 <= r < n):
+        raise SystemExit(f"bench.py: --share {share}: need 0 <= R < N")
+    return r, n
+
+
 def main_interp(args):
     import torch
 
-    world, rank, local, dist, dev = _dist_init()
+    share = parse_share(args.share) if args.share else None
+    if share is not None:
+        # one GPU, no process group: rank R's step of the N-rank strong partition
+        if env_world()[0] != 1 or args.scaling != "strong":
+            raise SystemExit("bench.py: --share runs one process on one GPU, for a strong-scaling config")
+        world0, rank0, local, dist, dev = _dist_init()
+        rank, world = share
+    else:
+        world, rank, local, dist, dev = _dist_init(args)
     from ptv_interpolation_amd import _lib, synth, zslab
 
     G, k = args.grid, args.k
@@ -393,7 +488,7 @@ def main_interp(args):
     if weak:
         P, Q = synth.sphere_pack(args.particles, G, z_tiles=world, z_tile=rank)
         cols = zslab.replicate_columns(cols_of(P, Q), dist)
-    elif rank == 0:
+    elif rank == 0 or dist is None:
         P, Q = synth.sphere_pack(args.particles, G)
         cols = zslab.broadcast_columns(cols_of(P, Q), dist)
     else:
@@ -473,17 +568,22 @@ def main_interp(args):
 
     # RCCL all-gather reassembly of the full field, once, reported apart from `value`
     gather_ms = None
-    if dist is not None and not args.no_allgather and all((b - a) == (z1 - z0) for a, b in
-                                                          [zslab.rank_slab(nz, world, r) for r in range(world)]):
+    if dist is not None and not args.no_allgather:
+        counts = [b - a for a, b in (((r * G, (r + 1) * G) if weak else zslab.rank_slab(nz, world, r))
+                                     for r in range(world))]
         try:
-            torch.cuda.synchronize(dev)
-            dist.barrier()
-            tg = time.perf_counter()
-            for o in out:
-                full = zslab.gather_field(o[hlo:hlo + (z1 - z0)], dist)
-                del full
-            torch.cuda.synchronize(dev)
-            gather_ms = (time.perf_counter() - tg) * 1e3
+            for it in range(2):  # the first all-gather sets RCCL's channels up: time the second
+                torch.cuda.synchronize(dev)
+                dist.barrier()
+                tg = time.perf_counter()
+                for o in out:
+                    full = allgather_padded(o[hlo:hlo + (z1 - z0)], counts, dist)
+                    del full
+                torch.cuda.synchronize(dev)
+                gather_ms = (time.perf_counter() - tg) * 1e3
+            t = torch.tensor([gather_ms], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            gather_ms = float(t.item())
         except Exception as e:  # the reassembly must never take the bench line down
             gather_ms = repr(e)[:200]
 
@@ -503,12 +603,12 @@ def main_interp(args):
             if radius:
                 kw["idw_radius"] = radius
             walls = []
-            os.environ["PTV_DEVICE"] = str(local)  # this rank's GPU only (launcher.devices())
-            for _ in range(2):  # first call allocates the context's host-path buffers
-                t = time.perf_counter()
-                with contextlib.redirect_stdout(io.StringIO()):
-                    ip.interpolate_field(df, grid, method=args.method, **kw)
-                walls.append(time.perf_counter() - t)
+            with pinned_device(local):  # this rank's GPU only (launcher.devices())
+                for _ in range(2):  # first call allocates the context's host-path buffers
+                    t = time.perf_counter()
+                    with contextlib.redirect_stdout(io.StringIO()):
+                        ip.interpolate_field(df, grid, method=args.method, **kw)
+                    walls.append(time.perf_counter() - t)
             hs = _lib.Context.get(local).stats
             e2e = {"wall_s": round(walls[-1], 3), "mvoxels_per_s": round(G ** 3 / walls[-1] / 1e6, 1),
                    "ms_h2d": round(hs["ms_h2d"], 2), "ms_device": round(hs["ms_total"] - hs["ms_h2d"] - hs["ms_d2h"], 2),
@@ -568,14 +668,18 @@ def main_interp(args):
         except Exception as e:  # the baseline must never take the GPU line down
             cpu = {"value": None, "error": repr(e)[:200]}
 
-    if rank == 0:
+    if rank == 0 or share is not None:
         vox_total = V_slab * world if weak else G ** 3
         value = vox_total / (elapsed / args.steps) / 1e6
+        if share is not None:  # one rank's share: its own slab's rate; the N-rank value is the rehearsal's
+            value = V_slab / (elapsed / args.steps) / 1e6
         if weak:
             wl = (f"{G}x{G}x{nz} grid = {world} stacked {G}^3 sphere-pack copies / {args.particles * world} "
                   f"particles (replicated), {G}^3 slab + {args.particles} particles' copy per GPU")
         else:
             wl = f"{G}^3 grid / {args.particles} particles (replicated), z-slab of {G // world if world else G} planes per GPU"
+        if share is not None:
+            wl = f"rank {rank} of {world}: planes [{z0}, {z1}) of the " + wl + " (one-GPU rehearsal, no collective)"
         if rbf:
             wl += f"; local RBF {kern} k={k} eps={eps} degree={deg} (system {m_sys}) fp64"
         else:
@@ -585,13 +689,17 @@ def main_interp(args):
                    (f" + sphere-pack fluid mask ({fluid_frac:.1%} fluid, solid skipped)" if args.mask else "") +
                    (" + consistent divergence (one-plane halo interpolated)" if args.div else ""))
         line = {
-            "metric": args.metric, "value": round(value, 2), "unit": "Mvoxels/s", "n_gpus": world,
+            "metric": args.metric, "value": round(value, 2), "unit": "Mvoxels/s",
+            "n_gpus": 1 if share is not None else world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f64",
+            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None,
+            # arithmetic type: every k-NN / weight / sum / solve is fp64; the C5 field is stored as f32
+            "dtype": "f64", "field_dtype": "f32" if out_f32 else "f64",
             "data": "synthetic: generate_sphere_pack.py geometry scaled to voxel units, seeded, w=1 flow field",
             "config": {"workload": wl, "name": args.config, "grid": G, "grid_z": nz, "particles": args.particles,
                        "particles_replicated": n, "method": args.method, "k": k, "power": args.power,
                        "out_dtype": "f32" if out_f32 else "f64", "mask": bool(args.mask), "div": bool(args.div),
+                       "planes": [z0, z1],
                        "parallelism": f"z-slab x{world}" + (" (particles replicated, slab_halo cull)" if cull else "")},
             "roofline": roof,
             "cpu_baseline": cpu,
@@ -599,10 +707,12 @@ def main_interp(args):
                              "lattice": round(avg["ms_lattice"], 3), "knn": round(avg["ms_knn"], 3),
                              "solve": round(avg["ms_solve"], 3), "divergence": round(avg["ms_stencil"], 3)},
         }
+        if share is not None:
+            line["share"] = {"rank": rank, "world": world}
         if args.mask:
             line["fluid_mvoxels_per_s"] = round(value * fluid_frac, 2)
         if cull:
-            line["halo"] = {**halo.as_dict(), "particles_binned_rank0": int(avg["n_binned"])}
+            line["halo"] = {**halo.as_dict(), "particles_binned": int(avg["n_binned"])}
         if gather_ms is not None:
             line["allgather_ms"] = round(gather_ms, 2) if isinstance(gather_ms, float) else gather_ms
         if e2e is not None:
@@ -637,20 +747,9 @@ def main_div(args):
     """--method div: one step = the consistent divergence of a resident (G, G, G) velocity field
     with the sphere-pack fluid mask (view_divergence.py:39).  Weak scaling: each rank owns a
     G^3 z-slab plus one halo plane per interior side (no collective on the data path)."""
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-
     import torch
 
-    dist = None
-    torch.cuda.set_device(local)
-    if world > 1:
-        import torch.distributed as dist
-
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    world, rank, local, dist, dev = _dist_init(args)
     from ptv_interpolation_amd import _lib, synth
 
     G = args.grid
@@ -735,7 +834,7 @@ def main_filter(args):
     Weak scaling: each rank filters its own sphere-pack copy (independent particle sets)."""
     import torch
 
-    world, rank, local, dist, dev = _dist_init()
+    world, rank, local, dist, dev = _dist_init(args)
     from ptv_interpolation_amd import _lib, synth
 
     k = 25 if args.k == 8 else args.k   # the reference default (main.py:44)
@@ -805,7 +904,7 @@ def main_mask(args):
     bytes.  Weak scaling: each rank processes its own mask copy."""
     import torch
 
-    world, rank, local, dist, dev = _dist_init()
+    world, rank, local, dist, dev = _dist_init(args)
     from ptv_interpolation_amd import _lib, synth
 
     G = args.grid
@@ -902,7 +1001,7 @@ def main_linear(args):
     import torch
     from scipy.spatial import Delaunay
 
-    world, rank, local, dist, dev = _dist_init()
+    world, rank, local, dist, dev = _dist_init(args)
     from ptv_interpolation_amd import _lib, synth
 
     G = args.grid if args.config != "headline" or args.grid != 512 else 256
@@ -979,8 +1078,64 @@ def main_linear(args):
         dist.destroy_process_group()
 
 
+def main_dryrun(args):
+    """--dry-run: the N-rank strong partition on the CPU over gloo.  Rank 0 generates the
+    particle set and broadcasts it, every rank computes its planes rank_slab(nz, N, r) (a fill
+    with the global plane index stands in for the HIP kernel, which needs a GPU), the padded
+    all-gather reassembles the field, and rank 0 checks that every plane arrived exactly once
+    and in order.  Prints one JSON line: world size, partition, check."""
+    import torch
+    import torch.distributed as dist
+
+    world, rank, _ = env_world()
+    check_world(args, world)
+    from ptv_interpolation_amd import synth, zslab
+
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo")
+    else:
+        dist = None
+    G = args.grid
+    nz = G
+    z0, z1 = zslab.rank_slab(nz, world, rank)
+    if rank == 0:
+        P, Q = synth.sphere_pack(args.particles, G)
+        cols = [torch.from_numpy(np.ascontiguousarray(a[:, i])) for a in (P, Q) for i in range(3)]
+    else:
+        cols = [torch.empty(args.particles, dtype=torch.float64) for _ in range(6)]
+    zslab.broadcast_columns(cols, dist)
+    digest = torch.tensor([float(sum(float(c.sum()) for c in cols))], dtype=torch.float64)
+    slab = torch.arange(z0, z1, dtype=torch.float64).view(-1, 1, 1).expand(z1 - z0, G, G).contiguous()
+    counts = [b - a for a, b in (zslab.rank_slab(nz, world, r) for r in range(world))]
+    full = zslab.gather_field(slab, dist, counts=counts)
+    digests = [torch.empty_like(digest) for _ in range(world)] if dist else [digest]
+    if dist:
+        dist.all_gather(digests, digest)
+    if rank == 0:
+        ok = (tuple(full.shape) == (nz, G, G) and
+              bool(torch.equal(full[:, 0, 0], torch.arange(nz, dtype=torch.float64))) and
+              bool(torch.equal(full, full[:, :1, :1].expand_as(full))))
+        print(json.dumps({"dry_run": True, "n_gpus": world, "world_size": dist.get_world_size() if dist else 1,
+                          "gpus_flag": args.gpus, "grid": G, "particles": args.particles,
+                          "partition": [list(zslab.rank_slab(nz, world, r)) for r in range(world)],
+                          "particles_agree": len({float(d.item()) for d in digests}) == 1,
+                          "field_reassembled": ok}), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.gpus is not None and args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        if args.share:
+            raise SystemExit("bench.py: --share is a one-GPU run; drop --gpus")
+        sys.exit(launch_ranks(args.gpus))
+    if args.dry_run:
+        return main_dryrun(args)
     if args.method == "linear":
         return main_linear(args)
     if args.method == "div":

@@ -644,11 +644,14 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
         }
     }
     PTV_TRY(prepare(c, &pe, g, &sp, ax, ay, az, qx, qy, qz, s, kl, b));
+    if (culled && kl.cb.dk == nullptr) {
+        // no lattice bounds were built, so nothing proves the cull exact: bin every particle
+        // instead (same result as slab_halo = 0), never refuse the call for it
+        culled = false;
+        c->cull_timed = false;
+        PTV_TRY(prepare(c, p, g, &sp, ax, ay, az, qx, qy, qz, s, kl, b));
+    }
     if (culled) {
-        if (kl.cb.dk == nullptr) {
-            set_error("slab cull: no lattice bounds to prove exactness");
-            return PTV_E_INEXACT;
-        }
         PTV_TRY(c->halo_need.ensure(1));
         PTV_TRY(launch_halo_need(kl.cb.ax, kl.cb.ay, kl.cb.az, kl.cb.n[0], kl.cb.n[1], kl.cb.n[2], kl.cb.dk,
                                  c->cull_win.p, kl.cg.mg, c->halo_need.p, s));
@@ -1119,8 +1122,9 @@ int ptv_interp_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const 
     PTV_TRY(host_call(c, p, g, prm->fluid_mask, nullptr, U, V, W,
                       [&](const ptv_particles *dp, const ptv_grid *dg, const uint8_t *dmask, const double *,
                           double *dU, double *dV, double *dW, hipStream_t s) {
+                          // st: on PTV_E_INEXACT the caller gets halo_required (host_call returns early)
                           return run_knn(c, dp, dg, prm, dg->ax, dg->ay, dg->az, dg->px, dg->py, dg->pz, dmask, dU,
-                                         dV, dW, s, nullptr);
+                                         dV, dW, s, st);
                       },
                       (prm->flags & PTV_FLAG_OUT_F32) ? sizeof(float) : sizeof(double)));
     if (st) *st = c->last;

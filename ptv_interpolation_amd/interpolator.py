@@ -180,17 +180,52 @@ def separable_axes(X, Y, Z):
     ay = np.ascontiguousarray(Y[0, :, 0], dtype=np.float64)
     az = np.ascontiguousarray(Z[:, 0, 0], dtype=np.float64)
 
-    def fits(A, ref, axis):
+    def zero_stride(A, axis):
         # zero-stride broadcast view (create_grid(dense=False)): constant along the two other
         # axes by construction, provided the one nonzero stride sits on `axis`
-        st = A.strides
-        if all(st[d] == 0 for d in range(3) if d != axis):
-            return True
-        return np.array_equal(A, np.broadcast_to(ref, A.shape))
+        return all(A.strides[d] == 0 for d in range(3) if d != axis)
 
-    if fits(X, ax[None, None, :], 2) and fits(Y, ay[None, :, None], 1) and fits(Z, az[:, None, None], 0):
+    checks = [(A, ref) for A, ref, axis in ((X, ax[None, None, :], 2), (Y, ay[None, :, None], 1),
+                                            (Z, az[:, None, None], 0)) if not zero_stride(A, axis)]
+    if not checks:
         return ax, ay, az
-    return None
+    # dense meshgrids (main.py:151 passes create_grid's): every element must match its axis
+    # value.  Cheap rejections first (corner planes), then the full comparison over z-chunks
+    # on a thread pool (numpy releases the GIL): 3 x 1 GiB at 512^3 read once, in parallel.
+    nz = X.shape[0]
+    for A, ref in checks:
+        for z in {0, nz - 1}:
+            if not np.array_equal(A[z], np.broadcast_to(ref[min(z, ref.shape[0] - 1)], A.shape[1:])):
+                return None
+    return (ax, ay, az) if _all_match(checks, nz) else None
+
+
+def _all_match(checks, nz):
+    """Whether every (A, ref) pair has A == broadcast(ref) elementwise, checked over z-chunks
+    on up to 16 threads with an early stop."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    plane = int(np.prod(checks[0][0].shape[1:]))
+    step = max(1, (1 << 21) // max(plane, 1))  # ~2M elements per task
+    chunks = [(a, min(nz, a + step)) for a in range(0, nz, step)]
+    bad = []
+
+    def run(ch):
+        if bad:
+            return
+        a, b = ch
+        for A, ref in checks:
+            r = ref[a:b] if ref.shape[0] > 1 else ref
+            if not np.array_equal(A[a:b], np.broadcast_to(r, A[a:b].shape)):
+                bad.append(ch)
+                return
+
+    if len(chunks) == 1:
+        run(chunks[0])
+    else:
+        with ThreadPoolExecutor(min(16, len(chunks), os.cpu_count() or 1)) as ex:
+            list(ex.map(run, chunks))
+    return not bad
 
 
 def _gpu_device():

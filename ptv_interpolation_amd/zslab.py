@@ -103,12 +103,31 @@ def halo_guess(n_particles: int, extent, k: int, factor: float = 4.0) -> float:
     return factor * r
 
 
-def gather_field(slab, dist=None):
-    """All-gather the ranks' equal-size (planes, ny, nx) slabs into the (world * planes, ny, nx)
-    field on every rank (RCCL over xGMI on the GPUs): the reassembly step, never on the data
-    path of the interpolation."""
+def gather_field(slab, dist=None, counts=None):
+    """All-gather the ranks' (planes_r, ny, nx) slabs into the (sum planes_r, ny, nx) field on
+    every rank (RCCL over xGMI on the GPUs): the reassembly step, never on the data path of the
+    interpolation.  ``counts``: every rank's plane count in rank order (default: all equal to
+    this slab's).  Unequal slabs are padded to the largest for one all_gather_into_tensor and
+    the padding is dropped afterwards."""
     if dist is None or dist.get_world_size() == 1:
         return slab
-    full = slab.new_empty((dist.get_world_size() * slab.shape[0],) + tuple(slab.shape[1:]))
-    dist.all_gather_into_tensor(full, slab.contiguous())
+    world = dist.get_world_size()
+    counts = [slab.shape[0]] * world if counts is None else [int(c) for c in counts]
+    if len(counts) != world or counts[dist.get_rank()] != slab.shape[0]:
+        raise ValueError(f"gather_field: counts {counts} do not match world {world} / this slab {slab.shape[0]}")
+    rest = tuple(slab.shape[1:])
+    pmax = max(counts)
+    if all(c == pmax for c in counts):
+        full = slab.new_empty((world * pmax,) + rest)
+        dist.all_gather_into_tensor(full, slab.contiguous())
+        return full
+    send = slab.new_zeros((pmax,) + rest)
+    send[:slab.shape[0]] = slab
+    padded = slab.new_empty((world * pmax,) + rest)
+    dist.all_gather_into_tensor(padded, send)
+    full = slab.new_empty((sum(counts),) + rest)
+    off = 0
+    for r, c in enumerate(counts):
+        full[off:off + c] = padded[r * pmax:r * pmax + c]
+        off += c
     return full

@@ -52,6 +52,60 @@ def boundary_ties(points, ax, ay, az, k):
     return (d[:, k - 1] == d[:, k]).reshape(X.shape)
 
 
+def hetero_ties_points(points, values, q, k, extra=8):
+    """(Q,) bool pair (tie, hetero) for query points q.
+
+    ``tie``: the k-th and (k+1)-th nearest particles are equidistant (the neighbour SET
+    depends on the search's tie order).  ``hetero``: such a voxel whose tied particles (every
+    particle at exactly the k-th distance) do not all carry the same (u, v, w); only there can
+    two correct searches give different results.  At a value-homogeneous tie every choice
+    gives identical terms (equal distances -> equal weights, equal values) in the same rank
+    order, so the result is bit-identical and the voxel stays in the comparison.  Tie runs
+    longer than the columns queried are re-queried with more neighbours (up to 1024 beyond k;
+    longer runs are counted heterogeneous, conservatively)."""
+    from scipy.spatial import KDTree
+
+    P = np.asarray(points, dtype=np.float64)
+    Vv = np.asarray(values, dtype=np.float64).reshape(len(P), -1)
+    q = np.asarray(q, dtype=np.float64).reshape(-1, 3)
+    kk = min(k + extra, len(P))
+    if kk <= k:
+        z = np.zeros(len(q), bool)
+        return z, z
+    tree = KDTree(P)
+    d, i = tree.query(q, k=kk, workers=-1)
+    d = d.reshape(len(q), -1)
+    tie = d[:, k - 1] == d[:, k]
+    hetero = np.zeros(len(q), bool)
+    rows = np.nonzero(tie)[0]
+    while len(rows):
+        dd, ii = tree.query(q[rows], k=kk, workers=-1)
+        dd = dd.reshape(len(rows), -1)
+        ii = ii.reshape(len(rows), -1)
+        again = []
+        for j, r in enumerate(rows):
+            at = dd[j] == dd[j, k - 1]
+            if at[-1] and kk < len(P):  # the tie run may continue past the columns queried
+                again.append(r)
+                continue
+            vals = Vv[ii[j, at]]
+            hetero[r] = bool(at[-1] and kk < len(P)) or not (vals == vals[0]).all()
+        if not again or kk >= min(len(P), k + 1024):
+            hetero[np.asarray(again, dtype=np.int64)] = True
+            break
+        rows = np.asarray(again)
+        kk = min(len(P), k + 4 * (kk - k))
+    return tie, hetero
+
+
+def hetero_ties(points, values, ax, ay, az, k):
+    """(tie, hetero) as (nz, ny, nx) bool over a separable grid (see hetero_ties_points)."""
+    Z, Y, X = np.meshgrid(az, ay, ax, indexing="ij")
+    q = np.stack([X.ravel(), Y.ravel(), Z.ravel()], -1)
+    tie, het = hetero_ties_points(points, values, q, k)
+    return tie.reshape(X.shape), het.reshape(X.shape)
+
+
 def filter_ties(points, k):
     """(n,) bool: particles whose remove_outliers_knn decision depends on cKDTree's tie order.
 

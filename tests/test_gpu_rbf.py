@@ -22,7 +22,7 @@ pytestmark = pytest.mark.gpu
 
 TOL = 1e-10
 TOL_ILL = 1e-8
-TRUTH_FACTOR = 2.0  # GPU distance to the exact answer vs the CPU LAPACKs' (see the Gaussian test)
+TRUTH_FACTOR = 1.0  # GPU distance to the exact answer vs the CPU LAPACKs' (see the Gaussian test)
 
 
 @pytest.fixture(scope="module")
