@@ -455,6 +455,48 @@ def parse_share(share):
     return r, n
 
 
+def e2e_leg(args, P, Q, G, k, radius, local):
+    """End to end through the drop-in, as main.py:151 + :184-192 call it: a host DataFrame
+    in, dense float64 create_grid meshgrids (3 x 8 V bytes), host float64 U, V, W out: the
+    separability check of the meshgrids, H2D, binning + kernels, D2H.  The first call also
+    creates the context and its device buffers (what a one-shot main.py run pays); the second
+    is the steady state.  Zero-stride create_grid(dense=False) views are timed as well."""
+    import pandas as pd
+
+    from ptv_interpolation_amd import _lib
+    from ptv_interpolation_amd import interpolator as ip
+
+    df = pd.DataFrame({"x": P[:, 0], "y": P[:, 1], "z": P[:, 2], "u": Q[:, 0], "v": Q[:, 1], "w": Q[:, 2]})
+    kw = {"idw": dict(idw_neighbors=k, idw_power=args.power), "sibson": dict(sibson_neighbors=k),
+          "nearest": {}}[args.method]
+    if radius:
+        kw["idw_radius"] = radius
+    res = {}
+    with pinned_device(local):  # this rank's GPU only (launcher.devices())
+        for name, dense in (("dense", True), ("views", False)):
+            grid, _ = ip.create_grid(((0, G), (0, G), (0, G)), G, dense=dense)
+            walls = []
+            for _ in range(2):
+                t = time.perf_counter()
+                with contextlib.redirect_stdout(io.StringIO()):
+                    out = ip.interpolate_field(df, grid, method=args.method, **kw)
+                walls.append(time.perf_counter() - t)
+                del out
+            hs = _lib.Context.get(local).stats
+            res[name] = {"wall_s_first": round(walls[0], 3), "wall_s": round(walls[-1], 3),
+                         "mvoxels_per_s": round(G ** 3 / walls[-1] / 1e6, 1),
+                         "ms_h2d": round(hs["ms_h2d"], 2),
+                         "ms_device": round(hs["ms_total"] - hs["ms_h2d"] - hs["ms_d2h"], 2),
+                         "ms_d2h": round(hs["ms_d2h"], 2)}
+            del grid
+    d = res["dense"]
+    d2h_floor = 3 * 8 * G ** 3 / 53e9 * 1e3  # measured pinned / touched D2H rate, 53 GB/s
+    return {**d, "views": res["views"], "d2h_floor_ms": round(d2h_floor, 1),
+            "what": "interpolate_field(DataFrame, create_grid() dense meshgrids as main.py:151) -> host float64 "
+                    "U, V, W; wall_s = second call, wall_s_first includes context + buffer creation; "
+                    "views = create_grid(dense=False)"}
+
+
 def main_interp(args):
     import torch
 
@@ -590,31 +632,9 @@ def main_interp(args):
     # end-to-end through the drop-in (host DataFrame in, host float64 U, V, W out): H2D +
     # binning + kernels + D2H, what a main.py user pays (N = 1, unmasked k-NN configs)
     e2e = None
-    if world == 1 and not rbf and not args.mask and not args.div and not args.no_e2e and P is not None:
+    if world == 1 and share is None and not rbf and not args.mask and not args.div and not args.no_e2e and P is not None:
         try:
-            import pandas as pd
-
-            from ptv_interpolation_amd import interpolator as ip
-
-            df = pd.DataFrame({"x": P[:, 0], "y": P[:, 1], "z": P[:, 2], "u": Q[:, 0], "v": Q[:, 1], "w": Q[:, 2]})
-            grid, _ = ip.create_grid(((0, G), (0, G), (0, G)), G, dense=False)
-            kw = {"idw": dict(idw_neighbors=k, idw_power=args.power), "sibson": dict(sibson_neighbors=k),
-                  "nearest": {}}[args.method]
-            if radius:
-                kw["idw_radius"] = radius
-            walls = []
-            with pinned_device(local):  # this rank's GPU only (launcher.devices())
-                for _ in range(2):  # first call allocates the context's host-path buffers
-                    t = time.perf_counter()
-                    with contextlib.redirect_stdout(io.StringIO()):
-                        ip.interpolate_field(df, grid, method=args.method, **kw)
-                    walls.append(time.perf_counter() - t)
-            hs = _lib.Context.get(local).stats
-            e2e = {"wall_s": round(walls[-1], 3), "mvoxels_per_s": round(G ** 3 / walls[-1] / 1e6, 1),
-                   "ms_h2d": round(hs["ms_h2d"], 2), "ms_device": round(hs["ms_total"] - hs["ms_h2d"] - hs["ms_d2h"], 2),
-                   "ms_d2h": round(hs["ms_d2h"], 2),
-                   "what": "interpolate_field(DataFrame, create_grid(dense=False)) -> host float64 U, V, W; "
-                           "pageable host buffers, second call"}
+            e2e = e2e_leg(args, P, Q, G, k, radius, local)
         except Exception as e:
             e2e = {"error": repr(e)[:200]}
 

@@ -293,6 +293,51 @@ def dev_dp(ptr: int):
     return C.cast(C.c_void_p(ptr), _dp)
 
 
+class ParticleColumns:
+    """The particle set as six contiguous float64 columns x, y, z, u, v, w (no copy when the
+    caller's columns already are, e.g. a DataFrame's float64 block rows)."""
+
+    def __init__(self, cols):
+        cols = [np.ascontiguousarray(c, dtype=np.float64).reshape(-1) for c in cols]
+        if len(cols) != 6 or len({len(c) for c in cols}) != 1:
+            raise ValueError("ParticleColumns: six equal-length columns x, y, z, u, v, w")
+        self.cols = cols
+        self.n = len(cols[0])
+
+    @classmethod
+    def from_frame(cls, df):
+        """x, y, z, u, v, w of a DataFrame coerced to float64 as interpolator.py:78-79 does."""
+        return cls([df[c].to_numpy(dtype=np.float64) for c in ("x", "y", "z", "u", "v", "w")])
+
+    @property
+    def points(self):
+        return np.stack(self.cols[:3], 1)
+
+    @property
+    def values(self):
+        return np.stack(self.cols[3:], 1)
+
+
+def _columns(points, values):
+    """Six contiguous float64 columns from (N, 3) points and values, or a ParticleColumns
+    passed as ``points`` (``values`` None)."""
+    if isinstance(points, ParticleColumns):
+        return list(points.cols)
+    pts = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 3)
+    vals = np.ascontiguousarray(values, dtype=np.float64).reshape(-1, 3)
+    return [np.ascontiguousarray(pts[:, i]) for i in range(3)] + [np.ascontiguousarray(vals[:, i]) for i in range(3)]
+
+
+def _into(out, res):
+    """``res`` copied into the caller's ``out`` arrays (same contract as _outputs) when given."""
+    if out is None:
+        return res
+    out = _outputs(out, res[0].shape, res[0].dtype)
+    for o, r in zip(out, res):
+        np.copyto(o, r)
+    return tuple(out)
+
+
 def _outputs(out, shape, dtype):
     """Three output arrays: the caller's (checked: C-contiguous, shape, dtype) or new ones."""
     if out is None:
@@ -406,13 +451,11 @@ class Context:
 
     def filter_outliers_knn(self, points, values, k=25, threshold=3.0, mad_eps=1e-6):
         """(keep uint8 (n,), kth_dist float64 (n,)) of the median/MAD k-NN filter."""
-        pts = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 3)
-        vals = np.ascontiguousarray(values, dtype=np.float64).reshape(-1, 3)
-        cols = [np.ascontiguousarray(pts[:, i]) for i in range(3)] + [np.ascontiguousarray(vals[:, i]) for i in range(3)]
-        P = Particles(pts.shape[0], *[as_dp(c) for c in cols])
+        cols = _columns(points, values)
+        P = Particles(len(cols[0]), *[as_dp(c) for c in cols])
         prm = FilterParams(int(k), float(threshold), float(mad_eps))
-        keep = np.empty(pts.shape[0], dtype=np.uint8)
-        kth = np.empty(pts.shape[0], dtype=np.float64)
+        keep = np.empty(len(cols[0]), dtype=np.uint8)
+        kth = np.empty(len(cols[0]), dtype=np.float64)
         st = Stats()
         check(lib().ptv_filter_outliers_knn(self.h, C.byref(P), C.byref(prm), keep.ctypes.data_as(_u8p),
                                             as_dp(kth), C.byref(st)))
@@ -463,10 +506,8 @@ class Context:
 
         ``out``: optional three C-contiguous (nz', ny, nx) arrays of the output dtype (e.g.
         z-slices of the caller's full arrays) written in place by the D2H."""
-        pts = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 3)
-        vals = np.ascontiguousarray(values, dtype=np.float64).reshape(-1, 3)
-        cols = [np.ascontiguousarray(pts[:, i]) for i in range(3)] + [np.ascontiguousarray(vals[:, i]) for i in range(3)]
-        P = Particles(pts.shape[0], *[as_dp(c) for c in cols])
+        cols = _columns(points, values)
+        P = Particles(len(cols[0]), *[as_dp(c) for c in cols])
         keep = list(cols)
         if axes is not None:
             ax, ay, az = (np.ascontiguousarray(a, dtype=np.float64).ravel() for a in axes)
@@ -481,8 +522,8 @@ class Context:
                 res = self.interp_knn(points, values, grid_points=gp, shape=tshape, method=method, k=k,
                                       power=power, eps=eps, fluid_mask=fm, flags=flags,
                                       cell_occupancy=cell_occupancy, r0_scale=r0_scale,
-                                      lattice_bounds=lattice_bounds, radius=radius)
-                return tuple(unpad(a) for a in res)
+                                      lattice_bounds=lattice_bounds, slab_halo=slab_halo, radius=radius)
+                return _into(out, tuple(unpad(a) for a in res))
             nz, ny, nx = shape
             keep += gp
             G = Grid(nx, ny, nz, None, None, None, as_dp(gp[0]), as_dp(gp[1]), as_dp(gp[2]), 0, nz)
@@ -511,10 +552,8 @@ class Context:
         """Host-array local RBF (scipy RBFInterpolator(neighbors=k) semantics; the arguments are
         already resolved by ptv_interpolation_amd.rbf).  ``smoothing``: scalar or (n,) array.
         Returns (U, V, W) float64 (nz', ny, nx)."""
-        pts = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 3)
-        vals = np.ascontiguousarray(values, dtype=np.float64).reshape(-1, 3)
-        cols = [np.ascontiguousarray(pts[:, i]) for i in range(3)] + [np.ascontiguousarray(vals[:, i]) for i in range(3)]
-        P = Particles(pts.shape[0], *[as_dp(c) for c in cols])
+        cols = _columns(points, values)
+        P = Particles(len(cols[0]), *[as_dp(c) for c in cols])
         keep = list(cols)
         if axes is not None:
             ax, ay, az = (np.ascontiguousarray(a, dtype=np.float64).ravel() for a in axes)
@@ -529,7 +568,7 @@ class Context:
                 res = self.interp_rbf(points, values, grid_points=gp, shape=tshape, k=k, kernel=kernel,
                                       epsilon=epsilon, degree=degree, smoothing=smoothing, fluid_mask=fm,
                                       flags=flags, chunk_planes=chunk_planes)
-                return tuple(unpad(a) for a in res)
+                return _into(out, tuple(unpad(a) for a in res))
             nz, ny, nx = shape
             keep += gp
             G = Grid(nx, ny, nz, None, None, None, as_dp(gp[0]), as_dp(gp[1]), as_dp(gp[2]), 0, nz)
@@ -559,10 +598,8 @@ class Context:
                       fluid_mask=None, flags=0, z_range=None, chunk_planes=0, out=None):
         """Host-array linear (Delaunay) interpolation (griddata(method='linear') semantics) over
         ``tri`` (a Triangulation of these points).  Returns (U, V, W) float64 (nz', ny, nx)."""
-        pts = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 3)
-        vals = np.ascontiguousarray(values, dtype=np.float64).reshape(-1, 3)
-        cols = [np.ascontiguousarray(pts[:, i]) for i in range(3)] + [np.ascontiguousarray(vals[:, i]) for i in range(3)]
-        P = Particles(pts.shape[0], *[as_dp(c) for c in cols])
+        cols = _columns(points, values)
+        P = Particles(len(cols[0]), *[as_dp(c) for c in cols])
         keep = list(cols)
         if axes is not None:
             ax, ay, az = (np.ascontiguousarray(a, dtype=np.float64).ravel() for a in axes)
@@ -576,7 +613,7 @@ class Context:
                 gp, tshape, fm, unpad = ft
                 res = self.interp_linear(points, values, tri, grid_points=gp, shape=tshape, fill_value=fill_value,
                                          fluid_mask=fm, flags=flags, chunk_planes=chunk_planes)
-                return tuple(unpad(a) for a in res)
+                return _into(out, tuple(unpad(a) for a in res))
             nz, ny, nx = shape
             keep += gp
             G = Grid(nx, ny, nz, None, None, None, as_dp(gp[0]), as_dp(gp[1]), as_dp(gp[2]), 0, nz)

@@ -77,7 +77,7 @@ def build(verbose: bool = False, force: bool = False) -> str:
     with ThreadPoolExecutor(max_workers=min(4, max(1, len(jobs)))) as ex:
         list(ex.map(run, jobs))
     if force or jobs or _stale(LIB, objs):
-        run([cc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", LIB])
+        run([cc, "-shared", "-fPIC", "-pthread", f"--offload-arch={ARCH}", *objs, "-o", LIB])
     return LIB
 
 

@@ -61,6 +61,10 @@ namespace ptv {
 #define PTV_KNN_WAVES_MID 3  // 8 < KMAX <= 32: capped for 3 waves per SIMD (Sibson k=30 and the RBF k=32 slot search -7 %)
 #endif
 
+#ifndef PTV_STAMP_ALL
+#define PTV_STAMP_ALL 0  // dev builds: 1 = the STAMP instantiation for every KMAX (not only 8)
+#endif
+
 constexpr int kStampFields = 8;
 constexpr int kCap = 128;        // LDS candidate slots per wave (16 B fp32 + 32 B fp64 each)
 constexpr int kRowsPerLane = 1;  // cell rows examined per lane per gather round
@@ -1318,7 +1322,7 @@ template <int KMAX, int MODE>
 static void launch_m(dim3 grid, hipStream_t s, const KnnKernelArgs &ka, const Binned &b, const double *ax,
                      const double *ay, const double *az, const double *qx, const double *qy, const double *qz,
                      const uint8_t *mask, double *U, double *V, double *W) {
-    if constexpr (KMAX == 8 && MODE != kModeSlots) {
+    if constexpr ((KMAX == 8 || PTV_STAMP_ALL) && MODE != kModeSlots) {
         // stamps record the main launch, or the lattice-level launches under PTV_STAMP_LATTICE=1
         const char *sl = std::getenv("PTV_STAMP_LATTICE");
         const int stamp_mode = (sl && sl[0] == '1') ? kModeKDist : kModeInterp;

@@ -238,7 +238,7 @@ def _knn_field(points, values, grid_tuple, method, k, power, radius=0.0):
     with X's shape."""
     X, Y, Z = grid_tuple
     shape = np.shape(X)
-    n = points.shape[0]
+    n = points.n if isinstance(points, _lib.ParticleColumns) else points.shape[0]
     if method == "idw_radius":
         # extension (no reference counterpart): k is not used
         if not (np.isfinite(radius) and radius > 0):
@@ -290,18 +290,20 @@ def interpolate_field(df, grid_tuple, method="linear", rbf_neighbors=20, rbf_ker
     against ``oracle.cpu_ref.idw_radius_points`` to 1e-12 normwise.
     """
     X, Y, Z = grid_tuple
-    points = np.asarray(df[["x", "y", "z"]].values, dtype=np.float64)
-    values = np.asarray(df[["u", "v", "w"]].values, dtype=np.float64)
+    # interpolator.py:78-79 (float64 coercion); the k-NN methods take the DataFrame's columns
+    # as they are (a float64 block's rows are contiguous: no (N, 3) gathers or column copies)
+    cols = _lib.ParticleColumns.from_frame(df)
 
     if method == "sibson":
         print(f"Using Sibson (Natural Neighbor) Interpolation (neighbors={sibson_neighbors})...")
-        return _knn_field(points, values, grid_tuple, "sibson", int(sibson_neighbors), 2.0)
+        return _knn_field(cols, None, grid_tuple, "sibson", int(sibson_neighbors), 2.0)
     if method == "idw" and idw_radius is not None:
         print(f"Using IDW Interpolation (power={idw_power}, radius={idw_radius})...")
-        return _knn_field(points, values, grid_tuple, "idw_radius", 1, float(idw_power), float(idw_radius))
+        return _knn_field(cols, None, grid_tuple, "idw_radius", 1, float(idw_power), float(idw_radius))
     if method == "idw":
         print(f"Using IDW Interpolation (power={idw_power}, neighbors={idw_neighbors})...")
-        return _knn_field(points, values, grid_tuple, "idw", int(idw_neighbors), float(idw_power))
+        return _knn_field(cols, None, grid_tuple, "idw", int(idw_neighbors), float(idw_power))
+    points, values = cols.points, cols.values
     if method == "rbf":
         print(f"Using RBF Interpolation ({rbf_kernel}) with {rbf_neighbors} neighbors, "
               f"smoothing={smoothing} and n_jobs={n_jobs}...")
@@ -312,7 +314,7 @@ def interpolate_field(df, grid_tuple, method="linear", rbf_neighbors=20, rbf_ker
     if method == "nearest":
         # griddata(method='nearest') (interpolator.py:196-197) is NearestNDInterpolator: the
         # k = 1 query of the same GPU k-NN kernel, values of the nearest particle
-        return _knn_field(points, values, grid_tuple, "nearest", 1, 2.0)
+        return _knn_field(cols, None, grid_tuple, "nearest", 1, 2.0)
     if method == "linear":
         return _linear_field(points, values, grid_tuple)
     # 'cubic' (and anything else) goes to griddata as in the reference, which raises for 3-D data

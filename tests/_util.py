@@ -55,10 +55,11 @@ def boundary_ties(points, ax, ay, az, k):
 def hetero_ties_points(points, values, q, k, extra=8):
     """(Q,) bool pair (tie, hetero) for query points q.
 
-    ``tie``: the k-th and (k+1)-th nearest particles are equidistant (the neighbour SET
-    depends on the search's tie order).  ``hetero``: such a voxel whose tied particles (every
-    particle at exactly the k-th distance) do not all carry the same (u, v, w); only there can
-    two correct searches give different results.  At a value-homogeneous tie every choice
+    ``tie``: two of the k + 1 nearest particles are equidistant (at the k-th distance the
+    neighbour SET depends on the search's tie order; below it the rank ORDER does, and numpy's
+    pairwise sum rounds differently in another order).  ``hetero``: such a voxel where some
+    run of equidistant neighbours touching the first k does not carry one (u, v, w); only there
+    can two correct searches give different bits.  At value-homogeneous ties every choice
     gives identical terms (equal distances -> equal weights, equal values) in the same rank
     order, so the result is bit-identical and the voxel stays in the comparison.  Tie runs
     longer than the columns queried are re-queried with more neighbours (up to 1024 beyond k;
@@ -69,13 +70,13 @@ def hetero_ties_points(points, values, q, k, extra=8):
     Vv = np.asarray(values, dtype=np.float64).reshape(len(P), -1)
     q = np.asarray(q, dtype=np.float64).reshape(-1, 3)
     kk = min(k + extra, len(P))
-    if kk <= k:
-        z = np.zeros(len(q), bool)
-        return z, z
     tree = KDTree(P)
     d, i = tree.query(q, k=kk, workers=-1)
     d = d.reshape(len(q), -1)
-    tie = d[:, k - 1] == d[:, k]
+    # any two of the first min(k + 1, n) neighbours at exactly the same distance: the order of
+    # equidistant neighbours (and, at the k-th, the set) is the search's choice
+    kb = min(k + 1, kk)
+    tie = (d[:, :kb - 1] == d[:, 1:kb]).any(axis=1)
     hetero = np.zeros(len(q), bool)
     rows = np.nonzero(tie)[0]
     while len(rows):
@@ -84,12 +85,22 @@ def hetero_ties_points(points, values, q, k, extra=8):
         ii = ii.reshape(len(rows), -1)
         again = []
         for j, r in enumerate(rows):
-            at = dd[j] == dd[j, k - 1]
-            if at[-1] and kk < len(P):  # the tie run may continue past the columns queried
+            if kk < len(P) and dd[j, -1] == dd[j, k - 1]:  # the k-th's tie run may continue
                 again.append(r)
                 continue
-            vals = Vv[ii[j, at]]
-            hetero[r] = bool(at[-1] and kk < len(P)) or not (vals == vals[0]).all()
+            # every run of equal distances touching ranks < k must carry one value: then any
+            # order (and any choice at the k-th) gives the same terms in the same rank order
+            bad = False
+            s = 0
+            while s < min(k, dd.shape[1]) and not bad:
+                e = s
+                while e + 1 < dd.shape[1] and dd[j, e + 1] == dd[j, s]:
+                    e += 1
+                if e > s:
+                    vals = Vv[ii[j, s:e + 1]]
+                    bad = not (vals == vals[0]).all()
+                s = e + 1
+            hetero[r] = bad
         if not again or kk >= min(len(P), k + 1024):
             hetero[np.asarray(again, dtype=np.int64)] = True
             break
