@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define PTV_API_VERSION 7
+#define PTV_API_VERSION 8
 
 /* error codes */
 #define PTV_OK 0
@@ -153,6 +153,8 @@ typedef struct {
     int64_t n_binned;    /* particles binned (after the slab_halo cull; = n_particles without) */
     double halo_required;/* slab_halo cull: the smallest halo this call proves exact (-1: no cull) */
     double ms_cull;      /* slab_halo cull + exactness check (inside ms_bin / before ms_knn) */
+    int64_t n_repair_tiles; /* k >= 13: 4x4x4 tiles rerun with exact (d2, slot) lists because two
+                             * distinct distances shared a packed key's truncation (ABI v8) */
 } ptv_stats;
 
 /*

@@ -119,7 +119,7 @@ class Stats(C.Structure):
                 ("n_cells", C.c_int64), ("cells", C.c_int32 * 3), ("cell_size", C.c_double * 3),
                 ("r0", C.c_double), ("ms_solve", C.c_double), ("n_singular", C.c_int64),
                 ("ms_stencil", C.c_double), ("n_binned", C.c_int64), ("halo_required", C.c_double),
-                ("ms_cull", C.c_double)]
+                ("ms_cull", C.c_double), ("n_repair_tiles", C.c_int64)]
 
     def as_dict(self):
         d = {f: getattr(self, f) for f, _ in self._fields_}

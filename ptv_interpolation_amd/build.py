@@ -19,7 +19,10 @@ CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 LIB = os.path.join(HERE, "libptv_amd.so")
 BUILD = os.path.join(HERE, "csrc", "_build")
-SOURCES = ["ptv_api.cpp", "ptv_bin.hip", "ptv_knn.hip", "ptv_rbf.hip", "ptv_div.hip", "ptv_mask.hip", "ptv_filter.hip", "ptv_linear.hip"]
+# the k-NN kernel's list lengths compile in parallel (ptv_knn_k*.hip instantiate ptv_knn_impl.hpp)
+KNN_PARTS = ["ptv_knn_k" + g + ".hip" for g in "abcdefgh"]
+SOURCES = (["ptv_api.cpp", "ptv_bin.hip", "ptv_knn.hip"] + KNN_PARTS +
+           ["ptv_rbf.hip", "ptv_div.hip", "ptv_mask.hip", "ptv_filter.hip", "ptv_linear.hip"])
 ARCH = os.environ.get("PTV_OFFLOAD_ARCH", "gfx950")
 # per-file extras: the local-RBF kernel keeps each voxel's system row in registers, so every
 # loop over the row must unroll fully (a partial unroll turns the row into scratch memory)
@@ -74,7 +77,10 @@ def build(verbose: bool = False, force: bool = False) -> str:
             raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
         return r
 
-    with ThreadPoolExecutor(max_workers=min(4, max(1, len(jobs)))) as ex:
+    workers = int(os.environ.get("PTV_BUILD_JOBS", str(min(16, os.cpu_count() or 4))))
+    # longest translation units first
+    jobs.sort(key=lambda cmd: -os.path.getsize(cmd[-3]))
+    with ThreadPoolExecutor(max_workers=max(1, min(workers, len(jobs)))) as ex:
         list(ex.map(run, jobs))
     if force or jobs or _stale(LIB, objs):
         run([cc, "-shared", "-fPIC", "-pthread", f"--offload-arch={ARCH}", *objs, "-o", LIB])

@@ -88,6 +88,8 @@ struct ptv_ctx {
     DevBuf<double> cull[6], cull_win;                            // slab cull: kept particles, z window
     DevBuf<uint32_t> cull_cnt;                                   // slab cull: per-block counts
     DevBuf<unsigned long long> halo_need;                        // slab cull: proven halo (double bits)
+    DevBuf<unsigned int> rep_cnt;                                // key-list near-tie repair: count
+    DevBuf<uint32_t> rep_list;                                   //   and the listed tiles
     hipEvent_t ev_div0 = nullptr, ev_div1 = nullptr;             // around the divergence stencil
     bool div_pending = false;
     std::vector<hipEvent_t> rbf_ev;                              // 3 per chunk: knn start, solve start, end
@@ -96,7 +98,7 @@ struct ptv_ctx {
     DevBuf<double> lin_tr;
     DevBuf<long long> lin_flags;                                 // linear: voxels left to the brute force
     double *h_bbox = nullptr;  // pinned, 6 doubles
-    unsigned long long *h_misc = nullptr;  // pinned scratch words (cull count, halo bound)
+    unsigned long long *h_misc = nullptr;  // pinned scratch words (cull count, halo bound, repair count)
     ptv_stats last{};
 };
 
@@ -185,7 +187,7 @@ int ptv_init(int device, ptv_ctx **out) {
     PTV_HIP(hipEventCreate(&c->ev_div0));
     PTV_HIP(hipEventCreate(&c->ev_div1));
     PTV_HIP(hipHostMalloc(&c->h_bbox, 8 * sizeof(double)));
-    PTV_HIP(hipHostMalloc(&c->h_misc, 4 * sizeof(unsigned long long)));
+    PTV_HIP(hipHostMalloc(&c->h_misc, 8 * sizeof(unsigned long long)));
     *out = c;
     return PTV_OK;
 }
@@ -241,6 +243,8 @@ int ptv_free(ptv_ctx *c) {
     c->cull_win.release();
     c->cull_cnt.release();
     c->halo_need.release();
+    c->rep_cnt.release();
+    c->rep_list.release();
     if (c->h_misc) hipHostFree(c->h_misc);
     hipEventDestroy(c->ev_main0);
     hipEventDestroy(c->ev_cull0);
@@ -588,6 +592,19 @@ int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchP
     ls.r0 = kl.r0;
     ls.n_binned = n;
     ls.halo_required = -1.0;
+    if (kmax_for(prm->k) >= 16) {
+        // packed-key lists: the near-tie repair list (tiles whose order the keys did not prove;
+        // a handful per launch: past the cap the whole launch reruns exact)
+        const long long tiles = (long long)((g->nx + 3) / 4) * ((g->ny + 3) / 4) * ((z1 - z0 + 3) / 4);
+        const int cap = (int)std::max<long long>(1, std::min<long long>(tiles, 1LL << 22));
+        PTV_TRY(c->rep_cnt.ensure(1));
+        PTV_TRY(c->rep_list.ensure((size_t)cap));
+        kl.rep_cnt = c->rep_cnt.p;
+        kl.rep_list = c->rep_list.p;
+        kl.rep_cap = cap;
+        kl.h_rep = reinterpret_cast<unsigned int *>(c->h_misc + 2);
+        kl.n_repair = &ls.n_repair_tiles;
+    }
     return PTV_OK;
 }
 
@@ -1539,7 +1556,7 @@ int filter_check(ptv_ctx *c, const ptv_particles *p, const ptv_filter_params *pr
         return PTV_E_ARG;
     }
     if (prm->k < 1 || filter_kmax(prm->k) == 0) {
-        set_error("filter: k must be in [1, 63]");
+        set_error("filter: k must be in [1, 126]");
         return PTV_E_UNSUPPORTED;
     }
     if (p->n <= prm->k) {

@@ -126,13 +126,8 @@ int launch_slot_speed(const double4 *pval, int64_t n, double *spd, hipStream_t s
     return PTV_OK;
 }
 
-int filter_kmax(int k) {
-    if (k <= 8) return 8;
-    if (k <= 16) return 16;
-    if (k <= 32) return 32;
-    if (k <= 63) return 64;
-    return 0;
-}
+// the (k+1)-NN list length serving the filter's k (0: unsupported)
+int filter_kmax(int k) { return k >= 1 ? kmax_for(k + 1) : 0; }
 
 int launch_binned_queries(const double4 *prec, int64_t n, int64_t npad, double *qx, double *qy, double *qz,
                           hipStream_t s) {

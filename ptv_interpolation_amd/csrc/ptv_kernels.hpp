@@ -75,6 +75,14 @@ struct KnnLaunch {
     double radius = 0.0;         // kModeRadius: the search radius
     FilterEpilogue fe;           // kModeFilter
     const int *order = nullptr;  // dispatch order of the launch's blocks (NULL: XCD-contiguous ranges)
+    // near-tie repair of the packed-key lists (k >= 13, modes interp / slots / filter): a device
+    // counter + tile list (rep_cap entries), a pinned host word for the count, and a counter of
+    // repaired tiles (stats, may be NULL)
+    unsigned int *rep_cnt = nullptr;
+    uint32_t *rep_list = nullptr;
+    int rep_cap = 0;
+    unsigned int *h_rep = nullptr;
+    int64_t *n_repair = nullptr;
 };
 
 // Longest-first dispatch order for a lattice-level k-NN launch over (nx, ny, nz) points: each

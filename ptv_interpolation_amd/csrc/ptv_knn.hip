@@ -1,1124 +1,11 @@
-// ptv_knn.hip — exact k-nearest-neighbour IDW / Sibson interpolation onto a voxel grid (gfx950).
-//
-// Replaces, per voxel, the reference hot loop
-//   distances, indices = tree.query(flat_coords, k)                 interpolator.py:139 (:97)
-//   weights = 1/(d**p + 1e-10); weights /= weights.sum(axis=1)       interpolator.py:142-147
-//   (Sibson: inv-distance * exp(-d/std(d)), renormalised            interpolator.py:102-116)
-//   out[:, c] = (weights * values[indices, c]).sum(axis=1)          interpolator.py:150-153 (:119-122)
-//
-// Work decomposition: one wave64 = one 4x4x4 voxel tile (lane = voxel); a 256-thread
-// workgroup = 4 independent tiles along x (16x4x4 voxels, 128-B output rows).
-//
-// Exact search by radius shells around the tile's bounding box B:
-//   pass 1 gathers every particle whose cell lies within R0 of B (R0 from the mean
-//   particle density); pass j gathers the shell R_{j-1} < dist <= R_j.  A lane whose
-//   current k-th distance is <= R_j is exact (every particle it has not seen is
-//   farther than R_j from B, hence from its voxel).  If all lists are full the next
-//   radius is the largest lane k-th distance (one more pass finishes every lane);
-//   otherwise R doubles.  Sphere interiors (empty voids) just take more passes.
-// Gather: the candidate cells of a pass are, per cell row (cy, cz), one or two x-runs
-// of consecutive cells = contiguous particle ranges of the linear-order counting sort.
-// Lane i takes row i: it loads its run bounds from cell_start (64 rows per round,
-// all loads in flight together), a wave prefix sum places the runs, and the lanes
-// copy the particle records into a per-wave LDS buffer.  The compute loop then reads
-// each candidate with a wave-uniform LDS address (broadcast) and updates every lane's
-// sorted register list of the KMAX best (d2, slot) with a branch-free insertion
-// network, skipped wave-wide when no lane improves.
-//
-// Bit-level contract with the reference (compiled with -ffp-contract=off):
-//   d2 = (dx*dx + dy*dy) + dz*dz, d = sqrt(d2)      (cKDTree p=2 accumulation, then sqrt)
-//   d**p: p=2 -> d*d, 1 -> d, 0.5 -> sqrt, -1 -> 1/d, else pow (numpy scalar fast paths)
-//   row sums: numpy pairwise order from identity 0.0 (8 accumulators, n%8 tail)
-// Ties at equal d2 keep the earlier candidate in the (deterministic) gather order
-// (cKDTree's tie order is traversal dependent too).
-#include <hip/hip_runtime.h>
-
-#include <cfloat>
-#include <cstdlib>
-#include <algorithm>
-#include <cmath>
-
-#include "../../include/ptv_api.h"
-#include "ptv_kernels.hpp"
-#include "ptv_median.hpp"
-#include "ptv_wave.hpp"
+// ptv_knn.hip — host side of the k-NN launches (list-length dispatch, near-tie repair) and the
+// lattice helper kernels; the k-NN kernel itself is ptv_knn_impl.hpp.
+#include "ptv_knn_impl.hpp"
 
 namespace ptv {
 
-#ifndef PTV_SUBBALL_RUNS
-#define PTV_SUBBALL_RUNS 1  // clip the gather runs to the sub-balls' chords (0: the tile ball's)
-#endif
-#ifndef PTV_KNN_WAVES
-#define PTV_KNN_WAVES 4  // waves per SIMD the k <= 8 kernels are register-capped for
-#endif
-#ifndef PTV_KNN_WAVES_BIG
-#define PTV_KNN_WAVES_BIG 2  // KMAX > 32: capped for 2 waves per SIMD (spills, yet k = 50 -30 %: one wave could not hide its latency)
-#endif
-#ifndef PTV_KNN_WAVES_SMALL
-#define PTV_KNN_WAVES_SMALL 5  // KMAX = 4 (nearest, radius, k <= 4): 5 waves per SIMD (nearest -2 %)
-#endif
-#ifndef PTV_KNN_WAVES_MID
-#define PTV_KNN_WAVES_MID 3  // 8 < KMAX <= 32: capped for 3 waves per SIMD (Sibson k=30 and the RBF k=32 slot search -7 %)
-#endif
-
-#ifndef PTV_STAMP_ALL
-#define PTV_STAMP_ALL 0  // dev builds: 1 = the STAMP instantiation for every KMAX (not only 8)
-#endif
-
-constexpr int kStampFields = 8;
-constexpr int kCap = 128;        // LDS candidate slots per wave (16 B fp32 + 32 B fp64 each)
-constexpr int kRowsPerLane = 1;  // cell rows examined per lane per gather round
-constexpr int kRunEntries = 64 * 2 * kRowsPerLane;  // x-runs per gather round (power of two)
-
-// Diagnostics (ptv_debug_stamps): when set, KMAX=8 launches use the STAMP instantiation,
-// which writes one record of kStampFields u64 per wave (s_memtime phase cycles + counts).
 unsigned long long *g_dbg = nullptr;
 long long g_dbg_cap = 0;  // records
-
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
-struct KnnKernelArgs {
-    CellGrid cg;
-    int nx, ny, nz, z0, z1;
-    int ntx, nty, ntz, ntxb;
-    int separable, method, k, kpad;
-    double power, eps;
-    uint32_t flags;
-    double r0;    // first gather radius
-    double rall;  // radius that covers the whole cell grid from any query
-    int mode;     // kModeInterp / kModeKDist
-    CoarseBound cb;
-    float4 *kd_recs;   // kModeKDist: k-NN seed records out (NULL = none): {p - c (fp32), slot}
-    int lz0;           // plane of coarse-lattice point 0
-    uint32_t *slots;   // kModeSlots: neighbour slots out
-    int seed_n;        // seed records used per lattice corner (<= k)
-    int nblocks;       // workgroups of the launch (the grid may be 2-D, see launch_knn)
-    double radius;     // kModeRadius: every particle with d2 <= radius^2 (query_ball_point's test)
-    FilterEpilogue fe;  // kModeFilter
-    const int *order;  // block dispatch order (NULL: XCD-contiguous ranges)
-};
-
-// numpy pairwise sum of a[0..n) (n <= KMAX <= 128), from identity 0.0.
-template <int KMAX>
-__device__ __forceinline__ double pairwise(const double (&a)[KMAX], int n) {
-    if (KMAX < 8 || n < 8) {
-        double r = 0.0;
-#pragma unroll
-        for (int j = 0; j < KMAX; ++j)
-            if (j < n) r += a[j];
-        return r;
-    }
-    if constexpr (KMAX >= 8) {
-        double r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3], r4 = a[4], r5 = a[5], r6 = a[6], r7 = a[7];
-        const int stop = n - (n & 7);
-#pragma unroll
-        for (int i = 8; i + 8 <= KMAX; i += 8) {
-            if (i < stop) {
-                r0 += a[i + 0];
-                r1 += a[i + 1];
-                r2 += a[i + 2];
-                r3 += a[i + 3];
-                r4 += a[i + 4];
-                r5 += a[i + 5];
-                r6 += a[i + 6];
-                r7 += a[i + 7];
-            }
-        }
-        double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-#pragma unroll
-        for (int j = 8; j < KMAX; ++j)
-            if (j >= stop && j < n) res += a[j];
-        return res;
-    }
-    return 0.0;
-}
-
-// numpy pairwise sum of t[j] = w[j] * values[bp[j], c] over j < n (n >= 1), streaming the
-// value loads in blocks of 8 (one block in flight at a time) instead of holding KMAX of them.
-// Same order as pairwise(): 8 accumulators seeded with t[0..7], blocks of 8, then the tail.
-template <int KMAX>
-__device__ __forceinline__ double gather_pairwise(const double (&w)[KMAX], const int (&bp)[KMAX],
-                                                  const double *__restrict__ vb, int c, int n) {
-    auto val = [&](int j) { return vb[(size_t)max(bp[j], 0) * 4 + c]; };
-    double v8[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v8[i] = val(i);
-    if (n < 8) {
-        double r = 0.0;
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-            if (i < n) r += w[i] * v8[i];
-        return r;
-    }
-    double r[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) r[i] = w[i] * v8[i];
-    const int stop = n - (n & 7);
-#pragma unroll
-    for (int m = 8; m + 8 <= KMAX; m += 8) {
-        if (m < stop) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) v8[i] = val(m + i);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) r[i] += w[m + i] * v8[i];
-        }
-    }
-    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-#pragma unroll
-    for (int j = 8; j < KMAX; ++j)
-        if (j >= stop && j < n) res += w[j] * val(j);
-    return res;
-}
-
-// d ** p with numpy's scalar fast paths (p uniform).
-__device__ __forceinline__ double np_pow(double d, double p) {
-    if (p == 2.0) return d * d;
-    if (p == 1.0) return d;
-    if (p == 0.5) return sqrt(d);
-    if (p == -1.0) return 1.0 / d;
-    return pow(d, p);
-}
-
-// a / b correctly rounded from r = RN(1/b): q = RN(a r), then q + RN(a - b q) r (Markstein; exact
-// for normal operands, checked against IEEE division on 3.6e8 random pairs).  One division
-// serves every numerator that shares the denominator.
-__device__ __forceinline__ double div_by(double a, double b, double r) {
-    const double q = a * r;
-    return fma(fma(-q, b, a), r, q);
-}
-
-// IEEE sqrt for x >= 2^-767: the LLVM gfx9 f64 expansion (rsq seed, two Goldschmidt
-// corrections) without its small-input rescale; tiny, zero and infinite x take sqrt()
-__device__ __forceinline__ double sqrt_cr(double x) {
-    if (!(x >= 0x1p-767 && x < INFINITY)) return sqrt(x);
-    const double y = __builtin_amdgcn_rsq(x);
-    double g = x * y, h = y * 0.5;
-    const double r = fma(-h, g, 0.5);
-    g = fma(g, r, g);
-    h = fma(h, r, h);
-    g = fma(fma(-g, g, x), h, g);
-    return fma(fma(-g, g, x), h, g);
-}
-
-// one voxel's outputs: float64, or float32 (RNE, numpy astype) under PTV_FLAG_OUT_F32
-__device__ __forceinline__ void store_out(uint32_t flags, double *U, double *V, double *W, size_t vo, double u,
-                                          double v, double w) {
-    if (flags & PTV_FLAG_OUT_F32) {
-        reinterpret_cast<float *>(U)[vo] = (float)u;
-        reinterpret_cast<float *>(V)[vo] = (float)v;
-        reinterpret_cast<float *>(W)[vo] = (float)w;
-    } else {
-        U[vo] = u;
-        V[vo] = v;
-        W[vo] = w;
-    }
-}
-
-__device__ __forceinline__ double nan_to_num(double v) {
-    if (v != v) return 0.0;
-    if (v == INFINITY) return DBL_MAX;
-    if (v == -INFINITY) return -DBL_MAX;
-    return v;
-}
-
-// a wave-uniform double held in SGPRs
-__device__ __forceinline__ double uniform(double v) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffffLL));
-    const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
-    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-
-__device__ __forceinline__ double wave_min(double v) { return group_reduce<0x3f>(v, OpMin{}); }
-__device__ __forceinline__ double wave_max(double v) { return group_reduce<0x3f>(v, OpMax{}); }
-__device__ __forceinline__ int wave_max_i(int v) { return group_reduce<0x3f>(v, OpMax{}); }
-__device__ __forceinline__ int wave_incl_max_scan_i(int v) { return wave_incl_scan_max(v); }
-__device__ __forceinline__ int wave_incl_scan_i(int v) { return wave_incl_scan_add(v); }
-
-// order this wave's LDS writes before its later reads (and vice versa)
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// v_min_f64 / v_max_f64 without the input canonicalisation fmin/fmax get in IEEE mode (the
-// list never holds NaN or signalling values)
-__device__ __forceinline__ double vmin_f64(double a, double b) {
-    double r;
-    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-__device__ __forceinline__ double vmax_f64(double a, double b) {
-    double r;
-    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-
-template <int KMAX>
-__device__ __forceinline__ void insert(double (&bd)[KMAX], int (&bp)[KMAX], double d2, int p) {
-    // Ascending carry sweep: m_j = d2 < bd[j] is monotone in j over the sorted list; from the
-    // first j where it holds, slot j takes the carry (the candidate, then each displaced
-    // entry) and hands its old entry on.  Ties keep the earlier entry first.  Every slot is
-    // updated in place (selects on v_cmp masks, no exec-mask branches).
-    // On a sorted list the carry is never below bd[j] once it differs from d2, so the distance
-    // slot is min(bd[j], carry) and the new carry the max (one op each).  One asm block per slot
-    // updates bd[j] and bp[j] IN PLACE (the carries go to fresh registers): written with
-    // separate selects, the compiler renamed the list every step and paid 14 moves per insert
-    // at the loop back-edge to put it back.
-    double cd = d2;
-    int cp = p;
-#pragma unroll
-    for (int j = 0; j < KMAX; ++j) {
-        if (j == KMAX - 1) {  // the last slot: no carry leaves the list
-            asm("v_cmp_lt_f64 vcc, %[d2], %[bd]\n\t"
-                "v_min_f64 %[bd], %[bd], %[cd]\n\t"
-                "v_cndmask_b32 %[bp], %[bp], %[cp], vcc"
-                : [bd] "+v"(bd[j]), [bp] "+v"(bp[j])
-                : [d2] "v"(d2), [cd] "v"(cd), [cp] "v"(cp)
-                : "vcc");
-            break;
-        }
-        double ncd;
-        int ncp;
-        asm("v_cmp_lt_f64 vcc, %[d2], %[bd]\n\t"
-            "v_max_f64 %[nc], %[bd], %[cd]\n\t"
-            "v_min_f64 %[bd], %[bd], %[cd]\n\t"
-            "v_cndmask_b32 %[np], %[cp], %[bp], vcc\n\t"
-            "v_cndmask_b32 %[bp], %[bp], %[cp], vcc"
-            : [bd] "+v"(bd[j]), [bp] "+v"(bp[j]), [nc] "=&v"(ncd), [np] "=&v"(ncp)
-            : [d2] "v"(d2), [cd] "v"(cd), [cp] "v"(cp)
-            : "vcc");
-        cd = ncd;
-        cp = ncp;
-    }
-}
-
-// min(a, b) for non-NaN operands without fmin's canonicalising v_max
-__device__ __forceinline__ double dmin(double a, double b) { return a < b ? a : b; }
-
-// fp32 prefilter threshold: every candidate whose exact d2 is < thr has fp32 d2 <= this
-// (thr < 0: inactive lane, never; thr = inf: everything).
-__device__ __forceinline__ float f32_bound(double thr, double cpass) {
-    if (thr < 0.0) return -1.0f;
-    return (float)((thr * (1.0 + 9.5367431640625e-07) + cpass) * (1.0 + 2.384185791015625e-07));
-}
-
-__device__ __forceinline__ int clampi(double f, int n) {
-    return f < 0.0 ? 0 : (f >= (double)(n - 1) ? n - 1 : (int)f);
-}
-
-// an upper bound on sqrt(x), x >= 0, from the fp32 square root (any over-estimate of a
-// gather half-width only adds cells; the same inputs always give the same bound)
-__device__ __forceinline__ float sqrtf_up(float x) {  // x >= 0 already rounded up
-    // v_sqrt_f32 (1 ulp) with 8 ulps of slack; inputs below 1e-30 are raised to it
-    return __builtin_amdgcn_sqrtf(fmaxf(x, 1e-30f)) * 1.0000005f;
-}
-__device__ __forceinline__ double sqrt_up(double x) {
-    return (double)sqrtf_up((float)(x * (1.0 + 2.384185791015625e-07)));
-}
-
-// bijection of [0, nb): block b (dispatched to XCD b % 8) -> a contiguous range per XCD
-__device__ __forceinline__ int xcd_block(int b, int nb) {
-    const int q = nb >> 3, r = nb & 7;
-    const int x = b & 7, i = b >> 3;
-    return (x < r) ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
-}
-
-// distance between the extent [lo, hi] of a query box and cell c of an axis
-__device__ __forceinline__ double axis_gap(int c, double o, double cs, double lo, double hi) {
-    const double c0 = o + (double)c * cs;
-    const double c1 = o + (double)(c + 1) * cs;
-    return fmax(fmax(c0 - hi, lo - c1), 0.0);
-}
-
-// MODE (kModeInterp / kModeKDist / kModeSlots) is a template parameter so that the search-only
-// modes carry no interpolation epilogue: one kernel for every mode put the KMAX = 32 lists at
-// 284 registers (one wave per SIMD); split, every KMAX <= 32 kernel runs two waves per SIMD.
-template <int KMAX, bool STAMP, int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
-    KMAX <= 4 ? PTV_KNN_WAVES_SMALL : (KMAX <= 8 ? PTV_KNN_WAVES : (KMAX <= 32 ? PTV_KNN_WAVES_MID : PTV_KNN_WAVES_BIG))))) void k_knn_interp(KnnKernelArgs a, const double4 *__restrict__ prec,
-                                                    const double4 *__restrict__ pval,
-                                                    const uint32_t *__restrict__ cstart,
-                                                    const double *__restrict__ ax, const double *__restrict__ ay,
-                                                    const double *__restrict__ az, const double *__restrict__ qpx,
-                                                    const double *__restrict__ qpy, const double *__restrict__ qpz,
-                                                    const uint8_t *__restrict__ mask, double *__restrict__ U,
-                                                    double *__restrict__ V, double *__restrict__ W,
-                                                    unsigned long long *__restrict__ dbg, long long dbg_cap) {
-    unsigned long long t_mark = 0, t_setup = 0, t_seed = 0, t_rows = 0, t_copy = 0, t_comp = 0, t_epi = 0;
-    auto stamp = [&](unsigned long long &acc) {
-        if constexpr (STAMP) {
-            const unsigned long long t = __builtin_amdgcn_s_memtime();
-            acc += t - t_mark;
-            t_mark = t;
-        }
-    };
-    if constexpr (STAMP) t_mark = __builtin_amdgcn_s_memtime();
-    __shared__ double4 lds_cand[4][kCap];
-    __shared__ __attribute__((aligned(16))) float lds_cfx[4][kCap], lds_cfy[4][kCap], lds_cfz[4][kCap];
-    __shared__ uint2 lds_runs[4][kRunEntries];
-    __shared__ int lds_owner[4][64];
-    // kModeRadius: the value records of the buffered candidates (the weights are summed in the flush)
-    __shared__ double4 lds_val[4][MODE == kModeRadius ? kCap : 1];
-    const int lane = threadIdx.x & 63;
-    const int wid = threadIdx.x >> 6;
-    double4 *buf = lds_cand[wid];
-    float *fbx = lds_cfx[wid], *fby = lds_cfy[wid], *fbz = lds_cfz[wid];
-    uint2 *runs = lds_runs[wid];
-    int *owner = lds_owner[wid];
-    // XCD-aware block order: the dispatcher deals workgroups round-robin over the 8 XCDs,
-    // so give XCD x a contiguous range of tiles (neighbouring tiles share cell rows and
-    // particle records; each XCD has its own L2)
-    const int lb = (int)(blockIdx.y * gridDim.x + blockIdx.x);  // linear dispatch order
-    if (lb >= a.nblocks) return;                                  // 2-D grid padding (block-uniform)
-    const int b = a.order != nullptr ? a.order[lb] : xcd_block(lb, a.nblocks);
-    const int bx = b % a.ntxb;
-    const int rr = b / a.ntxb;
-    const int ty = rr % a.nty;
-    const int tz = rr / a.nty;
-    const int tx = __builtin_amdgcn_readfirstlane(bx * 4 + wid);  // wave-uniform: scalar tile-box loads
-    if (tx >= a.ntx) return;  // wave-uniform
-    const int ix = tx * 4 + (lane & 3);
-    const int iy = ty * 4 + ((lane >> 2) & 3);
-    const int iz = a.z0 + tz * 4 + (lane >> 4);
-    const bool valid = ix < a.nx && iy < a.ny && iz < a.z1;
-    const int cx = min(ix, a.nx - 1), cy = min(iy, a.ny - 1), cz = min(iz, a.z1 - 1);
-    const size_t vfull = ((size_t)cz * a.ny + cy) * a.nx + cx;
-    double qx, qy, qz;
-    if (a.separable) {
-        qx = ax[cx];
-        qy = ay[cy];
-        qz = az[cz];
-    } else {
-        qx = qpx[vfull];
-        qy = qpy[vfull];
-        qz = qpz[vfull];
-    }
-    const bool active = valid && (mask == nullptr || mask[vfull] != 0);
-    // seed records (k-NN lists of the tile's 8 lattice corners: lane = corner * 8 + entry, each
-    // {particle - corner in fp32, slot}, 16 B), issued first so that their latency overlaps the
-    // lattice-bound loads below
-    float4 seed = make_float4(0.f, 0.f, 0.f, __uint_as_float(0xffffffffu));
-    double scx = 0.0, scy = 0.0, scz = 0.0;  // the lane's corner
-    if constexpr (KMAX <= 8) {
-        if (a.cb.recs != nullptr) {
-            const int jx0 = __builtin_amdgcn_readfirstlane(cx >> kLatticeShift);
-            const int jy0 = __builtin_amdgcn_readfirstlane(cy >> kLatticeShift);
-            const int jz0 = __builtin_amdgcn_readfirstlane((cz - a.lz0) >> kLatticeShift);
-            const int cc = lane >> 3, j = lane & 7;
-            const int jx = min(jx0 + (cc & 1), a.cb.n[0] - 1);
-            const int jy = min(jy0 + ((cc >> 1) & 1), a.cb.n[1] - 1);
-            const int jz = min(jz0 + (cc >> 2), a.cb.n[2] - 1);
-            if (j < a.seed_n) seed = a.cb.recs[(((size_t)jz * a.cb.n[1] + jy) * a.cb.n[0] + jx) * a.k + j];
-            scx = a.cb.ax[jx];
-            scy = a.cb.ay[jy];
-            scz = a.cb.az[jz];
-        }
-    }
-
-    // upper bound on this voxel's k-th distance from the coarse lattice (triangle inequality)
-    auto lattice_ub = [&]() -> double {
-        double u = INFINITY;
-        if (a.cb.dk == nullptr || !active) return u;
-        // |v - c| in fp32 from lattice-relative offsets, rounded up: any upper bound is valid
-        // the tile is one lattice cell: its corners are wave-uniform (scalar loads)
-        const int j0[3] = {__builtin_amdgcn_readfirstlane(cx >> kLatticeShift),
-                           __builtin_amdgcn_readfirstlane(cy >> kLatticeShift),
-                           __builtin_amdgcn_readfirstlane((cz - a.lz0) >> kLatticeShift)};
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            const int jx = min(j0[0] + (c & 1), a.cb.n[0] - 1);
-            const int jy = min(j0[1] + ((c >> 1) & 1), a.cb.n[1] - 1);
-            const int jz = min(j0[2] + (c >> 2), a.cb.n[2] - 1);
-            const float ex = (float)(qx - a.cb.ax[jx]), ey = (float)(qy - a.cb.ay[jy]), ez = (float)(qz - a.cb.az[jz]);
-            const float e2 = __fmaf_rn(ez, ez, __fmaf_rn(ey, ey, ex * ex));
-            const double D = a.cb.dk[((size_t)jz * a.cb.n[1] + jy) * a.cb.n[0] + jx];
-            u = fmin(u, D + (double)(sqrtf_up(e2) * 1.000002f));
-        }
-        return u * (1.0 + 1e-9) + a.cg.mg;
-    };
-    // With seed records the seeds' bound is the tighter one for (nearly) every lane: the
-    // D(c) + |v - c| bound is then formed only when some active lane got no seed bound.
-    bool seeds_defer = false;
-    if constexpr (KMAX <= 8) seeds_defer = a.cb.recs != nullptr;
-    double ub = seeds_defer ? INFINITY : lattice_ub();
-    // candidates at or beyond the bound can never be among the k nearest
-    double ub2 = !active ? -1.0 : (ub < INFINITY ? ub * ub : INFINITY);
-    // radius mode: every candidate with d2 <= R^2 counts (the list stays unused)
-    const double rad2 = a.radius * a.radius;
-    double rs = 0.0, rsu = 0.0, rsv = 0.0, rsw = 0.0;  // sum w, sum w*u, sum w*v, sum w*w
-    if constexpr (MODE == kModeRadius) ub2 = !active ? -1.0 : rad2 * (1.0 + 2.220446049250313e-16) + 1e-300;
-
-    // sorted list: KMAX-k front sentinels (-1) so bd[KMAX-1] is the k-th best.
-    // Inactive lanes (padding / solid voxels) hold -1 everywhere: they never accept a
-    // candidate and never ask for a larger radius.
-    double bd[KMAX];
-    int bp[KMAX];
-#pragma unroll
-    for (int j = 0; j < KMAX; ++j) {
-        bd[j] = (!active || j < a.kpad) ? -1.0 : INFINITY;
-        bp[j] = -1;
-    }
-    double thr = dmin(bd[KMAX - 1], ub2);
-
-    uint32_t n_pass = 0, n_round = 0, n_rows = 0, n_cand = 0, n_acc = 0, n_surv = 0;
-
-    stamp(t_setup);
-    if (__builtin_amdgcn_ballot_w64(active) != 0) {
-        // tile box (the gather geometry): on separable grids the extents of the tile's <= 4
-        // axis values (wave-uniform loads; padded and masked voxels only enlarge it), otherwise
-        // wave reductions over the active voxels
-        double bx0, bx1, by0, by1, bz0, bz1;
-        if (a.separable) {
-            auto ext = [](const double *axv, int i0, int imax, double &lo, double &hi) {
-                const double v0 = axv[i0], v1 = axv[min(i0 + 1, imax)], v2 = axv[min(i0 + 2, imax)],
-                             v3 = axv[min(i0 + 3, imax)];
-                lo = uniform(fmin(fmin(v0, v1), fmin(v2, v3)));
-                hi = uniform(fmax(fmax(v0, v1), fmax(v2, v3)));
-            };
-            ext(ax, tx * 4, a.nx - 1, bx0, bx1);
-            ext(ay, ty * 4, a.ny - 1, by0, by1);
-            ext(az, a.z0 + tz * 4, a.z1 - 1, bz0, bz1);
-        } else {
-            bx0 = uniform(wave_min(active ? qx : INFINITY));
-            bx1 = uniform(wave_max(active ? qx : -INFINITY));
-            by0 = uniform(wave_min(active ? qy : INFINITY));
-            by1 = uniform(wave_max(active ? qy : -INFINITY));
-            bz0 = uniform(wave_min(active ? qz : INFINITY));
-            bz1 = uniform(wave_max(active ? qz : -INFINITY));
-        }
-        const CellGrid &g = a.cg;
-        // tile centre: candidates and voxels get fp32 coordinates relative to it
-        const double tcx = uniform(0.5 * (bx0 + bx1)), tcy = uniform(0.5 * (by0 + by1)), tcz = uniform(0.5 * (bz0 + bz1));
-        const float qfx = (float)(qx - tcx), qfy = (float)(qy - tcy), qfz = (float)(qz - tcz);
-        const f32x2 qf2x = {qfx, qfx}, qf2y = {qfy, qfy}, qf2z = {qfz, qfz};
-        const double bhalf = 0.5 * sqrt_up(((bx1 - bx0) * (bx1 - bx0) + (by1 - by0) * (by1 - by0)) + (bz1 - bz0) * (bz1 - bz0));
-        bool seeded = false;
-        if constexpr (KMAX <= 8) {
-            if (a.cb.recs != nullptr) {
-                // ---- seeds: the k-NN lists of the tile's 8 coarse-lattice corners.  Every lane's
-                //      k-th smallest distance to their (deduplicated) union bounds its k-th
-                //      neighbour distance from above, usually to within a few ulps, so the gather
-                //      radius is tight and one pass is exact. ----
-                // deduplicate through an LDS hash table (the candidate buffer, unused yet): every
-                // lane writes its id at its slot's hash and keeps the slot if its own id is read
-                // back.  Equal slots -> one survivor; distinct slots that collide -> one survivor
-                // too, which only drops a seed: any subset of k distinct particles still bounds.
-                uint32_t *tab = reinterpret_cast<uint32_t *>(buf);
-                const uint32_t sl = __float_as_uint(seed.w);
-                const bool has = sl != 0xffffffffu;
-                const uint32_t hsh = (sl * 2654435761u) >> 22;  // 1024 entries = the 4 KB buffer
-                if (has) tab[hsh] = (uint32_t)lane;
-                wave_lds_sync();
-                const bool uniq = has && tab[hsh] == (uint32_t)lane;
-                const unsigned long long um = __builtin_amdgcn_ballot_w64(uniq);
-                const int nu = __builtin_popcountll(um);
-                const int pos = __builtin_amdgcn_mbcnt_hi((unsigned)(um >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)um, 0u));
-                double pm = 0.0;
-                if (uniq) {
-                    // particle - tile centre = (particle - corner) + (corner - centre): three fp32
-                    // roundings of magnitude <= Ms (covered by dl below)
-                    const float ex = seed.x + (float)(scx - tcx), ey = seed.y + (float)(scy - tcy),
-                                ez = seed.z + (float)(scz - tcz);
-                    fbx[pos] = ex;
-                    fby[pos] = ey;
-                    fbz[pos] = ez;
-                    // >= the Euclidean distance to the centre (fp32 sum rounded up)
-                    pm = ((double)fabsf(ex) + (double)fabsf(ey) + (double)fabsf(ez)) * (1.0 + 1e-6);
-                }
-                // seed-voxel distances are <= Ms; fp32 coordinate + distance error <= Ms * 2^-19
-                const double Ms = uniform(wave_max(pm)) + bhalf;
-                wave_lds_sync();
-                float sd[KMAX];
-#pragma unroll
-                for (int q = 0; q < KMAX; ++q) sd[q] = INFINITY;
-                for (int i = 0; i < nu; i += 2) {
-                    const float2 X = *reinterpret_cast<const float2 *>(fbx + i);
-                    const float2 Y = *reinterpret_cast<const float2 *>(fby + i);
-                    const float2 Z = *reinterpret_cast<const float2 *>(fbz + i);
-                    const f32x2 ex = qf2x - f32x2{X.x, X.y}, ey = qf2y - f32x2{Y.x, Y.y}, ez = qf2z - f32x2{Z.x, Z.y};
-                    f32x2 s2 = ex * ex;
-                    s2 = __builtin_elementwise_fma(ey, ey, s2);
-                    s2 = __builtin_elementwise_fma(ez, ez, s2);
-                    const float xs[2] = {s2.x, i + 1 < nu ? s2.y : INFINITY};
-#pragma unroll
-                    for (int u = 0; u < 2; ++u) {
-#pragma unroll
-                        for (int q = KMAX - 1; q > 0; --q) sd[q] = __builtin_amdgcn_fmed3f(sd[q - 1], sd[q], xs[u]);
-                        sd[0] = fminf(sd[0], xs[u]);
-                    }
-                }
-                float kth = sd[0];
-#pragma unroll
-                for (int q = 1; q < KMAX; ++q)
-                    if (q == a.k - 1) kth = sd[q];
-                if (active && kth < INFINITY) {
-                    const double dl = Ms * 1.9073486328125e-06;
-                    const double st2 = ((double)kth * (1.0 + 9.5367431640625e-07) + (2.0 * Ms * dl + dl * dl)) * (1.0 + 1e-12);
-                    if (st2 < ub2) {
-                        ub2 = st2;
-                        ub = sqrt_up(st2);
-                    }
-                }
-                if (__builtin_amdgcn_ballot_w64(active && !(kth < INFINITY)) != 0) {
-                    // rare (fewer than k distinct seeds survived the hash): the lattice bound
-                    const double u = lattice_ub();
-                    if (u < ub) {
-                        ub = u;
-                        ub2 = u * u;
-                    }
-                }
-                seeded = true;
-                thr = dmin(bd[KMAX - 1], ub2);
-                wave_lds_sync();  // the gather reuses the candidate buffers
-                stamp(t_seed);
-            }
-        }
-        double cpass = 0.0;
-        float thrf = 0.f;
-        double Rp = -1.0;  // radius already gathered (none yet)
-        // R_ub covers every lane's k-th neighbour: small (fluid) -> try r0 first and then
-        // the exact max k-th distance; large (void) -> one pass at R_ub.
-        const double R_ub = uniform(wave_max(active ? ub : -INFINITY));
-        double R = a.r0;
-        // a tight lattice bound (fine level) is used directly in one pass; a loose one
-        // (coarse level) is preceded by a pass at the density radius r0.
-        if (R_ub < INFINITY) R = (seeded || R_ub <= 2.0 * a.r0) ? R_ub : a.r0;
-        if constexpr (MODE == kModeRadius) R = a.radius;  // one pass
-        // ---- sub-balls: the tile's 8 sub-boxes of 2x2x2 voxels (lanes differing in bits 0, 2, 4),
-        //      each with centre c_s and radius max_v sqrt(thr_v) + |v - c_s|: a candidate outside
-        //      every sub-ball can never enter any list (thresholds only shrink), so the copy drops it.
-        //      fp32 on tile-relative coordinates, inflated for round-off (any over-estimate is safe).
-        float sbx[2], sby[2], sbz[2], sbr2[8];  // sub-box s spans x-half s&1, y-half s>>1&1, z-half s>>2
-        float sb_hd;                              // this lane's sub-box half-diagonal (rounded up)
-        {
-            // extent of this lane's x-half (lanes agreeing in bit 1), y-half (bit 3), z-half (bit 5)
-            const float mnx = group_reduce<0x3d>(qfx, OpMin{}), mxx = group_reduce<0x3d>(qfx, OpMax{});
-            const float mny = group_reduce<0x37>(qfy, OpMin{}), mxy = group_reduce<0x37>(qfy, OpMax{});
-            const float mnz = group_reduce<0x1f>(qfz, OpMin{}), mxz = group_reduce<0x1f>(qfz, OpMax{});
-            const float ux = mxx - mnx, uy = mxy - mny, uz = mxz - mnz;
-            sb_hd = 0.5f * sqrtf_up(__fmaf_rn(uz, uz, __fmaf_rn(uy, uy, ux * ux)) * 1.000001f) * 1.00001f;
-            const float cxs = 0.5f * (mnx + mxx), cys = 0.5f * (mny + mxy), czs = 0.5f * (mnz + mxz);
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                sbx[h] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cxs), h << 1));
-                sby[h] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cys), h << 3));
-                sbz[h] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(czs), h << 5));
-            }
-        }
-        double Mpass = 0.0;  // bound on |coordinate - tile centre| of this pass's candidates
-        auto subballs = [&]() {
-            // radius of sub-ball s: max over its 8 lanes of sqrt(thr) + the half-diagonal
-            float rv = thr < 0.0 ? -1.0f : sqrtf_up((float)(thr * (1.0 + 2.384185791015625e-07)));
-            rv = group_reduce<0x15>(rv, OpMax{});
-            const float Rs = (rv + sb_hd) * 1.00001f + (float)(Mpass * 1e-6);
-            const float R2s = rv < 0.0f ? -1.0f : Rs * Rs;
-#pragma unroll
-            for (int sb = 0; sb < 8; ++sb) {
-                const int L = ((sb & 1) << 1) | ((sb & 2) << 2) | ((sb & 4) << 3);
-                sbr2[sb] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(R2s), L));
-            }
-        };
-        int nbuf = 0;  // compacted candidates waiting in this wave's LDS buffer (uniform)
-        // ---- every buffered candidate against all 64 voxels, in groups of 32 candidates:
-        //      (1) a branch-free fp32 stream on tile-relative coordinates leaves each lane a bit
-        //          mask of the candidates that may beat its threshold;
-        //      (2) each lane then walks its own bits in candidate order: exact fp64 d2 and the
-        //          insertion network.  The wave runs (2) max-over-lanes-popcount times instead of
-        //          once per candidate any lane accepts. ----
-        auto flush = [&]() {
-            if (nbuf == 0) return;
-            wave_lds_sync();
-            for (int g0 = 0; g0 < nbuf; g0 += 64) {
-                const int ng = min(64, nbuf - g0);
-                // candidate g0 + j ends at bit nb - 1 - j (shift-in order keeps the loop rolled)
-                unsigned long long m = 0ull;
-                const int nb = (ng + 3) & ~3;
-#pragma unroll 1
-                for (int i0 = 0; i0 < ng; i0 += 4) {
-                    // 4 candidates as two packed-fp32 pairs (v_pk_add / v_pk_mul / v_pk_fma);
-                    // slots past nbuf hold stale values, their bits are cleared below
-                    const float4 X = *reinterpret_cast<const float4 *>(fbx + g0 + i0);
-                    const float4 Y = *reinterpret_cast<const float4 *>(fby + g0 + i0);
-                    const float4 Z = *reinterpret_cast<const float4 *>(fbz + g0 + i0);
-                    const f32x2 e0x = qf2x - f32x2{X.x, X.y}, e1x = qf2x - f32x2{X.z, X.w};
-                    const f32x2 e0y = qf2y - f32x2{Y.x, Y.y}, e1y = qf2y - f32x2{Y.z, Y.w};
-                    const f32x2 e0z = qf2z - f32x2{Z.x, Z.y}, e1z = qf2z - f32x2{Z.z, Z.w};
-                    f32x2 s0 = e0x * e0x, s1 = e1x * e1x;
-                    s0 = __builtin_elementwise_fma(e0y, e0y, s0);
-                    s1 = __builtin_elementwise_fma(e1y, e1y, s1);
-                    s0 = __builtin_elementwise_fma(e0z, e0z, s0);
-                    s1 = __builtin_elementwise_fma(e1z, e1z, s1);
-                    const uint32_t b4 = ((s0.x <= thrf) ? 8u : 0u) | ((s0.y <= thrf) ? 4u : 0u) |
-                                        ((s1.x <= thrf) ? 2u : 0u) | ((s1.y <= thrf) ? 1u : 0u);
-                    m = (m << 4) | b4;
-                }
-                m &= ~((1ull << (nb - ng)) - 1ull);  // stale slots past nbuf
-                const double4 *gbuf = buf + g0 + nb - 64;  // bit position p <-> gbuf[63 - p]
-                const int nit = __builtin_amdgcn_readfirstlane(wave_max_i(__builtin_popcountll(m)));
-                for (int it = 0; it < nit; ++it) {
-                    // branch-free body (lanes without bits read a valid stale slot and insert inf)
-                    ++n_acc;
-                    const bool has = m != 0ull;
-                    const int lz = __builtin_clzll(m | 1ull);
-                    m &= ~(0x8000000000000000ull >> lz);
-                    const double4 c = gbuf[lz];
-                    const double dx = qx - c.x, dy = qy - c.y, dz = qz - c.z;
-                    const double e2 = (dx * dx + dy * dy) + dz * dz;
-                    if constexpr (MODE == kModeRadius) {
-                        // IDW term of a particle inside the ball (cKDTree's d2 <= r*r test)
-                        if (has && active && e2 <= rad2) {
-                            const double4 val = lds_val[wid][gbuf - buf + lz];
-                            const double w = 1.0 / (np_pow(sqrt_cr(e2), a.power) + a.eps);
-                            rs += w;
-                            rsu += w * val.x;
-                            rsv += w * val.y;
-                            rsw += w * val.z;
-                        }
-                    } else {
-                        const double d2 = (has && e2 < thr) ? e2 : INFINITY;
-                        insert<KMAX>(bd, bp, d2, (int)__double_as_longlong(c.w));  // no-op where d2 = inf
-                        thr = dmin(bd[KMAX - 1], ub2);
-                    }
-                }
-                thrf = f32_bound(thr, cpass);
-            }
-            n_surv += (uint32_t)nbuf;
-            nbuf = 0;
-            wave_lds_sync();  // the buffer is refilled next
-            subballs();
-            stamp(t_comp);
-        };
-        int py0 = 1, py1 = 0, pz0 = 1, pz1 = 0;  // row box of the previous pass (empty)
-        while (true) {
-            ++n_pass;
-            const double Rg = R + g.mg, Rg2 = Rg * Rg;
-            {
-                // |fp32 - exact| distance error <= delta = M * 2^-21 for coordinates within M of the
-                // tile centre; (s + delta)^2 <= s^2 + 2 M delta + delta^2 bounds the test.
-                const double M = Rg + 2.0 * bhalf + 2.0 * fmax(g.cs[0], fmax(g.cs[1], g.cs[2]));
-                const double delta = M * 4.76837158203125e-07;
-                cpass = 2.0 * M * delta + delta * delta;
-                thrf = f32_bound(thr, cpass);
-                Mpass = M;
-                subballs();
-            }
-            const double Rpg2 = Rp < 0.0 ? -1.0 : (Rp + g.mg) * (Rp + g.mg);
-            const int ry0 = clampi(floor((by0 - Rg - g.o[1]) * g.ic[1]), g.nc[1]);
-            const int ry1 = clampi(floor((by1 + Rg - g.o[1]) * g.ic[1]), g.nc[1]);
-            const int rz0 = clampi(floor((bz0 - Rg - g.o[2]) * g.ic[2]), g.nc[2]);
-            const int rz1 = clampi(floor((bz1 + Rg - g.o[2]) * g.ic[2]), g.nc[2]);
-            // rows are visited centre-out (zigzag in y within zigzag in z around the tile's
-            // cell) so that near candidates come first and the k-th distances tighten early
-            const int cyc = clampi(floor((tcy - g.o[1]) * g.ic[1]), g.nc[1]);
-            const int czc = clampi(floor((tcz - g.o[2]) * g.ic[2]), g.nc[2]);
-            const int hy = max(cyc - ry0, ry1 - cyc), hz = max(czc - rz0, rz1 - czc);
-            const int nyr = 2 * hy + 1;
-            const int nrows = nyr * (2 * hz + 1);
-            const float inv_nyr = 1.0f / (float)nyr;
-            for (int rb = 0; rb < nrows; rb += 64 * kRowsPerLane) {
-                ++n_round;
-                // ---- lane = kRowsPerLane cell rows: x-runs of this shell -> particle ranges ----
-                uint32_t rs[2 * kRowsPerLane];
-                int rc[2 * kRowsPerLane];
-#pragma unroll
-                for (int q = 0; q < kRowsPerLane; ++q) {
-                    const int row = rb + q * 64 + lane;
-                    rs[2 * q] = rs[2 * q + 1] = 0;
-                    rc[2 * q] = rc[2 * q + 1] = 0;
-                    if (row < nrows) {
-                        int rq = (int)((float)row * inv_nyr);  // row / nyr without an integer divide
-                        rq -= (rq * nyr > row) ? 1 : 0;
-                        rq += ((rq + 1) * nyr <= row) ? 1 : 0;
-                        const int ty = row - rq * nyr;
-                        const int ccy = cyc + ((ty & 1) ? ((ty + 1) >> 1) : -(ty >> 1));
-                        const int ccz = czc + ((rq & 1) ? ((rq + 1) >> 1) : -(rq >> 1));
-                        const double gy = axis_gap(ccy, g.o[1], g.cs[1], by0, by1);
-                        const double gz = axis_gap(ccz, g.o[2], g.cs[2], bz0, bz1);
-                        const double h2 = gy * gy + gz * gz;
-                        if (h2 <= Rg2 && ccy >= ry0 && ccy <= ry1 && ccz >= rz0 && ccz <= rz1) {
-                            const double rx = sqrt_up(Rg2 - h2);
-                            const int a1 = clampi(floor((bx0 - rx - g.o[0]) * g.ic[0]), g.nc[0]);
-                            const int b1 = clampi(floor((bx1 + rx - g.o[0]) * g.ic[0]), g.nc[0]);
-                            int lo1 = a1, hi1 = b1, lo2 = 1, hi2 = 0;  // [lo, hi] inclusive runs
-                            if (h2 <= Rpg2 && ccy >= py0 && ccy <= py1 && ccz >= pz0 && ccz <= pz1) {
-                                // row was gathered by the previous pass: only the x extensions are new
-                                const double rxo = sqrt_up(Rpg2 - h2);
-                                const int a0 = clampi(floor((bx0 - rxo - g.o[0]) * g.ic[0]), g.nc[0]);
-                                const int b0 = clampi(floor((bx1 + rxo - g.o[0]) * g.ic[0]), g.nc[0]);
-                                hi1 = a0 - 1;
-                                lo2 = b0 + 1;
-                                hi2 = b1;
-                            }
-                            // both runs' bounds in flight together (an empty run reads cell 0 twice)
-#if PTV_SUBBALL_RUNS
-                            {
-                                // clip the runs to the union of the 8 sub-balls' chords of this row: a
-                                // particle that can enter any list lies in some sub-ball (the copy filter
-                                // below), so cells outside every chord are never needed.  fp32 on
-                                // tile-relative coordinates, every rounding widened (em).
-                                const float em = (float)(Mpass * 1e-6) + 1e-6f;
-                                const float ylo = (float)(g.o[1] + (double)ccy * g.cs[1] - tcy) - em;
-                                const float yhi = (float)(g.o[1] + (double)(ccy + 1) * g.cs[1] - tcy) + em;
-                                const float zlo = (float)(g.o[2] + (double)ccz * g.cs[2] - tcz) - em;
-                                const float zhi = (float)(g.o[2] + (double)(ccz + 1) * g.cs[2] - tcz) + em;
-                                float xl = INFINITY, xh = -INFINITY;
-#pragma unroll
-                                for (int sb = 0; sb < 8; ++sb) {
-                                    const float cyv = sby[(sb >> 1) & 1], czv = sbz[sb >> 2];
-                                    const float gy = fmaxf(fmaxf(ylo - cyv, cyv - yhi), 0.f);
-                                    const float gz = fmaxf(fmaxf(zlo - czv, czv - zhi), 0.f);
-                                    const float h2s = __fmaf_rn(gz, gz, gy * gy);
-                                    if (h2s <= sbr2[sb]) {
-                                        const float hw = sqrtf_up(fmaxf(sbr2[sb] - h2s, 0.f) + sbr2[sb] * 1e-6f);
-                                        xl = fminf(xl, sbx[sb & 1] - hw);
-                                        xh = fmaxf(xh, sbx[sb & 1] + hw);
-                                    }
-                                }
-                                if (xl <= xh) {
-                                    const int s0 = clampi(floor((tcx + (double)(xl - em) - g.o[0]) * g.ic[0]), g.nc[0]);
-                                    const int s1 = clampi(floor((tcx + (double)(xh + em) - g.o[0]) * g.ic[0]), g.nc[0]);
-                                    lo1 = max(lo1, s0);
-                                    hi1 = min(hi1, s1);
-                                    lo2 = max(lo2, s0);
-                                    hi2 = min(hi2, s1);
-                                } else {
-                                    hi1 = lo1 - 1;
-                                    hi2 = lo2 - 1;
-                                }
-                            }
-#endif
-                            const uint32_t *rp = cstart + ((long long)ccz * g.nc[1] + ccy) * g.nc[0];
-                            const bool e1 = lo1 <= hi1, e2 = lo2 <= hi2;
-                            const uint32_t s1 = rp[e1 ? lo1 : 0], t1 = rp[e1 ? hi1 + 1 : 0];
-                            const uint32_t s2 = rp[e2 ? lo2 : 0], t2 = rp[e2 ? hi2 + 1 : 0];
-                            rs[2 * q] = s1;
-                            rc[2 * q] = (int)(t1 - s1);
-                            rs[2 * q + 1] = s2;
-                            rc[2 * q + 1] = (int)(t2 - s2);
-                            ++n_rows;
-                        }
-                    }
-                }
-                int cnt = 0;
-#pragma unroll
-                for (int r = 0; r < 2 * kRowsPerLane; ++r) cnt += rc[r];
-                const int incl = wave_incl_scan_i(cnt);
-                const int off = incl - cnt;
-                const int total = __builtin_amdgcn_readlane(incl, 63);
-                // run table in LDS: entry lane*R+r = (first candidate index, first particle slot)
-#pragma unroll
-                for (int r = 0, pre = off; r < 2 * kRowsPerLane; ++r) {
-                    runs[lane * 2 * kRowsPerLane + r] = make_uint2((uint32_t)pre, rs[r]);
-                    pre += rc[r];
-                }
-                wave_lds_sync();
-                stamp(t_rows);
-                // ---- copy windows [src, src + 64) of this round's candidates.  Each run marks its
-                //      first window position with its id (ids grow with candidate order), a prefix
-                //      max gives every lane its run; lane i takes candidate src + i and keeps it
-                //      only if it lies in some sub-ball (compacted into the LDS buffer).  Software
-                //      pipelined: the next window's records are in flight while this one is filtered.
-                auto window_slot = [&](int src) -> uint32_t {
-                    owner[lane] = -1;
-                    wave_lds_sync();
-#pragma unroll
-                    for (int r = 0, pre = off; r < 2 * kRowsPerLane; ++r) {
-                        if (rc[r] > 0 && pre < src + 64 && pre + rc[r] > src)
-                            owner[max(pre, src) - src] = lane * 2 * kRowsPerLane + r;
-                        pre += rc[r];
-                    }
-                    wave_lds_sync();
-                    const int o = wave_incl_max_scan_i(owner[lane]);
-                    uint32_t sl = 0;  // lanes past the end read record 0 and drop it
-                    if (src + lane < total) {
-                        const uint2 rn = runs[o];
-                        sl = rn.y + (uint32_t)(src + lane - (int)rn.x);
-                    }
-                    return sl;
-                };
-                uint32_t next_slot = total > 0 ? window_slot(0) : 0u;
-                double4 next_rec = prec[next_slot];
-                for (int src = 0; src < total; src += 64) {
-                    const uint32_t slot = next_slot;
-                    const double4 p4 = next_rec;
-                    if (src + 64 < total) {
-                        next_slot = window_slot(src + 64);
-                        next_rec = prec[next_slot];
-                    }
-                    const int i = src + lane;
-                    bool keep = false;
-                    float ex = 0.f, ey = 0.f, ez = 0.f;
-                    if (i < total) {
-                        ex = (float)(p4.x - tcx);
-                        ey = (float)(p4.y - tcy);
-                        ez = (float)(p4.z - tcz);
-                        float qx2[2], qy2[2], qz2[2];
-#pragma unroll
-                        for (int h = 0; h < 2; ++h) {
-                            const float dx = ex - sbx[h], dy = ey - sby[h], dz = ez - sbz[h];
-                            qx2[h] = dx * dx;
-                            qy2[h] = dy * dy;
-                            qz2[h] = dz * dz;
-                        }
-#pragma unroll
-                        for (int sb = 0; sb < 8; ++sb)
-                            keep = keep || (qx2[sb & 1] + qy2[(sb >> 1) & 1]) + qz2[sb >> 2] <= sbr2[sb];
-                    }
-                    const unsigned long long km = __builtin_amdgcn_ballot_w64(keep);
-                    if (keep) {
-                        const int pos = nbuf + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(km >> 32),
-                                                                              __builtin_amdgcn_mbcnt_lo((unsigned)km, 0u));
-                        buf[pos] = make_double4(p4.x, p4.y, p4.z, __longlong_as_double((long long)slot));
-                        if constexpr (MODE == kModeRadius) lds_val[wid][pos] = pval[slot];
-                        fbx[pos] = ex;
-                        fby[pos] = ey;
-                        fbz[pos] = ez;
-                    }
-                    nbuf += __builtin_popcountll(km);
-                    n_cand += (uint32_t)min(64, total - src);
-                    stamp(t_copy);
-                    if (nbuf > kCap - 64) flush();
-                }
-            }
-            flush();
-            // ---- exactness: lanes with k-th distance <= R are final ----
-            const double worst = uniform(wave_max(bd[KMAX - 1]));  // inactive lanes hold -1
-            if (MODE == kModeRadius || worst <= R * R || R >= a.rall) break;
-            Rp = R;
-            py0 = ry0;
-            py1 = ry1;
-            pz0 = rz0;
-            pz1 = rz1;
-            if (worst < INFINITY) {
-                R = sqrt(worst) * (1.0 + 1e-12);  // every list full: one exact pass left
-            } else if (R_ub < INFINITY && R < R_ub) {
-                R = R_ub;  // the coarse-lattice bound covers every lane
-            } else {
-                // some list not full.  Void tiles: grow geometrically while nothing has been
-                // found (rows only, no candidates), then in small steps so that the last
-                // shell does not overshoot the lens of particles the voxels actually need.
-                bool seen = false;
-#pragma unroll
-                for (int j = 0; j < KMAX; ++j) seen = seen || bp[j] >= 0;
-                const bool any_seen = __builtin_amdgcn_ballot_w64(seen) != 0;
-                R = any_seen ? R + fmax(a.r0, 0.125 * R) : 1.5 * R;
-            }
-            R = fmin(R, a.rall);
-        }
-    }
-    stamp(t_setup);  // exactness checks / radius updates count as setup
-
-    // per-wave stamp record (ptv_debug_stamps), written by the first valid lane
-    auto write_stamps = [&]() {
-        if constexpr (STAMP) {
-            stamp(t_epi);
-            const long long gw = (long long)lb * 4 + wid;
-            if (dbg != nullptr && gw < dbg_cap && (threadIdx.x & 63) == (int)__builtin_ffsll((long long)__builtin_amdgcn_ballot_w64(true)) - 1) {
-                unsigned long long *r = dbg + gw * kStampFields;
-                r[0] = t_setup;
-                r[1] = t_seed;
-                r[2] = t_rows;
-                r[3] = t_copy;
-                r[4] = t_comp;
-                r[5] = t_epi;
-                r[6] = n_cand + ((unsigned long long)n_acc << 32);
-                r[7] = (n_round & 0xffffu) + ((unsigned long long)(n_pass & 0xffffu) << 16) + ((unsigned long long)n_surv << 32);
-            }
-        }
-    };
-    if (!valid) return;
-    const size_t vo = ((size_t)(iz - a.z0) * a.ny + iy) * a.nx + ix;
-    if constexpr (MODE == kModeKDist) {
-        U[vo] = sqrt(bd[KMAX - 1]);
-        if (a.kd_recs != nullptr) {
-            // the k-NN records (list order) seed the next finer level's tiles: {p - this lattice
-            // point in fp32, slot}
-            float4 *o = a.kd_recs + vo * (size_t)a.k;
-            double4 rec[KMAX];
-#pragma unroll
-            for (int j = 0; j < KMAX; ++j) rec[j] = prec[max(bp[j], 0)];  // every load in flight at once
-#pragma unroll
-            for (int j = 0; j < KMAX; ++j) {
-                if (j >= a.kpad) {
-                    const bool ok = bp[j] >= 0;
-                    o[j - a.kpad] = make_float4(ok ? (float)(rec[j].x - qx) : 0.f, ok ? (float)(rec[j].y - qy) : 0.f,
-                                                ok ? (float)(rec[j].z - qz) : 0.f,
-                                                __uint_as_float(ok ? (uint32_t)bp[j] : 0xffffffffu));
-                }
-            }
-        }
-        write_stamps();
-        return;
-    }
-    if constexpr (MODE == kModeFilter) {
-        // remove_outliers_knn (filtering.py:20-51) for the query particle of this lane: its k+1
-        // nearest (the list, slots kpad..KMAX-1, ascending), minus "the point itself" (column 0
-        // of the reference's query: the query's own record when it is in the list, the nearest
-        // otherwise), the neighbours' speeds, median and MAD, the keep test, and the (k+1)-th
-        // distance (printed median, :33-35)
-        const uint32_t orig = a.fe.q_orig[vfull];
-        if (!active || orig == 0xffffffffu) return;
-        const uint32_t qslot = a.fe.inv[orig];
-        const double dk1 = sqrt(bd[KMAX - 1]);  // the (k+1)-th distance
-        // left-shift the list by kpad (uniform) so the k+1 entries occupy slots 0..k
-#pragma unroll
-        for (int sh = 1; sh < KMAX; sh <<= 1) {
-            if (a.kpad & sh) {
-#pragma unroll
-                for (int j = 0; j + sh < KMAX; ++j) bp[j] = bp[j + sh];
-            }
-        }
-        const int k1 = a.k, kk = a.k - 1;  // k1 = k + 1 listed, kk = k neighbours without the point
-        int drop = 0;
-        double v[KMAX];
-#pragma unroll
-        for (int j = 0; j < KMAX; ++j) {
-            if (j < k1 && (uint32_t)bp[j] == qslot) drop = j;
-            v[j] = j < k1 ? a.fe.spd[max(bp[j], 0)] : 0.0;  // every gather in flight together
-        }
-        double sp[KMAX];
-#pragma unroll
-        for (int t = 0; t < KMAX; ++t) sp[t] = t + 1 < KMAX ? (t < drop ? v[t] : v[t + 1]) : 0.0;
-        const double med = median_of(sp, kk);
-        double dev[KMAX];
-#pragma unroll
-        for (int t = 0; t < KMAX; ++t) dev[t] = fabs(sp[t] - med);
-        const double mad = median_of(dev, kk);
-        const double zsc = fabs(a.fe.spd[qslot] - med) / (mad + a.fe.mad_eps);
-        a.fe.keep[orig] = zsc <= a.fe.threshold ? 1 : 0;
-        if (a.fe.kth != nullptr) a.fe.kth[orig] = dk1;
-        return;
-    }
-    if constexpr (MODE == kModeSlots) {
-        // the k neighbour slots (list order) for the local-RBF solve (ptv_rbf.hip)
-        if (!active) return;
-        uint32_t *o = a.slots + vo * (size_t)a.k;
-#pragma unroll
-        for (int j = 0; j < KMAX; ++j)
-            if (j >= a.kpad) o[j - a.kpad] = (uint32_t)bp[j];
-        return;
-    }
-    if (!active) {
-        store_out(a.flags, U, V, W, vo, 0.0, 0.0, 0.0);
-        return;
-    }
-    if constexpr (MODE == kModeRadius) {
-        // sum_j w_j u_j / sum_j w_j (an empty ball gives 0 / 0 = NaN, "no data")
-        double o[3] = {rsu / rs, rsv / rs, rsw / rs};
-        if (a.flags & PTV_FLAG_NAN_TO_NUM) {
-#pragma unroll
-            for (int c = 0; c < 3; ++c) o[c] = nan_to_num(o[c]);
-        }
-        store_out(a.flags, U, V, W, vo, o[0], o[1], o[2]);
-        return;
-    }
-
-    // left-shift the list by kpad so real entries occupy slots 0..k-1 (kpad uniform)
-#pragma unroll
-    for (int sh = 1; sh < KMAX; sh <<= 1) {
-        if (a.kpad & sh) {
-#pragma unroll
-            for (int j = 0; j + sh < KMAX; ++j) {
-                bd[j] = bd[j + sh];
-                bp[j] = bp[j + sh];
-            }
-        }
-    }
-    const int k = a.k;
-    if (a.method == PTV_METHOD_NEAREST) {
-        // griddata(method='nearest') (interpolator.py:196-197): NearestNDInterpolator returns
-        // values[i] of the single nearest particle (k = 1 query), no arithmetic
-        const double4 r = pval[max(bp[0], 0)];
-        const bool fix = (a.flags & PTV_FLAG_NAN_TO_NUM) != 0;
-        store_out(a.flags, U, V, W, vo, fix ? nan_to_num(r.x) : r.x, fix ? nan_to_num(r.y) : r.y,
-                  fix ? nan_to_num(r.z) : r.z);
-        return;
-    }
-    // k <= 8: the neighbours' value records are all loaded here, before the weight
-    // arithmetic below, so their latency overlaps it (slots past k are clamped to a valid
-    // record).  Larger lists stream them per component after the weights (register budget).
-    constexpr int KV = KMAX <= 8 ? KMAX : 1;
-    double pvu[KV], pvv[KV], pvw[KV];
-#pragma unroll
-    for (int j = 0; j < KV; ++j) {
-        const double4 r = pval[max(bp[j], 0)];
-        pvu[j] = r.x;
-        pvv[j] = r.y;
-        pvw[j] = r.z;
-    }
-    double w[KMAX];
-    if (a.method == PTV_METHOD_SIBSON) {
-        // interpolator.py:106-116
-        double d[KMAX], t[KMAX];
-#pragma unroll
-        for (int j = 0; j < KMAX; ++j) {
-            d[j] = (j < k) ? sqrt_cr(bd[j]) : 0.0;
-            t[j] = (j < k) ? 1.0 / (d[j] + a.eps) : 0.0;
-        }
-        const double s_inv = pairwise<KMAX>(t, k);
-        const double mean = pairwise<KMAX>(d, k) / (double)k;
-#pragma unroll
-        for (int j = 0; j < KMAX; ++j) {
-            w[j] = t[j] / s_inv;
-            const double c = d[j] - mean;
-            t[j] = c * c;
-        }
-        const double sd = sqrt(pairwise<KMAX>(t, k) / (double)k);
-        const double den = sd + a.eps;
-#pragma unroll
-        for (int j = 0; j < KMAX; ++j) w[j] = (j < k) ? w[j] * exp(-d[j] / den) : 0.0;
-        const double s2 = pairwise<KMAX>(w, k);
-#pragma unroll
-        for (int j = 0; j < KMAX; ++j) w[j] = w[j] / s2;
-    } else {
-        // interpolator.py:143-147
-#pragma unroll
-        for (int j = 0; j < KMAX; ++j) {
-            const double d = sqrt_cr(bd[j]);
-            w[j] = (j < k) ? 1.0 / (np_pow(d, a.power) + a.eps) : 0.0;
-        }
-        const double s = pairwise<KMAX>(w, k);
-        // w_j / s through one reciprocal when s and every quotient are normal (w_j > 0 here:
-        // s <= 2^1000 and min_j w_j >= s 2^-1000); IEEE division on any lane otherwise
-        double wmin = w[0];
-#pragma unroll
-        for (int j = 1; j < KMAX; ++j)
-            if (j < k) wmin = fmin(wmin, w[j]);
-        const bool fast = s <= 0x1p1000 && wmin >= s * 0x1p-1000;
-        if (__builtin_amdgcn_ballot_w64(!fast) == 0) {
-            const double rs = 1.0 / s;
-#pragma unroll
-            for (int j = 0; j < KMAX; ++j) w[j] = div_by(w[j], s, rs);
-        } else {
-#pragma unroll
-            for (int j = 0; j < KMAX; ++j) w[j] = w[j] / s;
-        }
-    }
-
-    // interpolator.py:150-153: per component, sum_k w * values[idx, c]
-    double out[3];
-    if constexpr (KMAX <= 8) {
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            double t[KMAX];
-#pragma unroll
-            for (int j = 0; j < KMAX; ++j) t[j] = (j < k) ? w[j] * (c == 0 ? pvu[j] : (c == 1 ? pvv[j] : pvw[j])) : 0.0;
-            out[c] = pairwise<KMAX>(t, k);
-        }
-    } else {
-        const double *vb = reinterpret_cast<const double *>(pval);
-#pragma unroll 1
-        for (int c = 0; c < 3; ++c) out[c] = gather_pairwise<KMAX>(w, bp, vb, c, k);
-    }
-    if (a.flags & PTV_FLAG_NAN_TO_NUM) {
-#pragma unroll
-        for (int c = 0; c < 3; ++c) out[c] = nan_to_num(out[c]);
-    }
-    store_out(a.flags, U, V, W, vo, out[0], out[1], out[2]);
-    write_stamps();
-}
 
 // ---------------------------------------------------------------------------
 // Count-only k-th distance UPPER bound (coarsest lattice).  One wave per grid point;
@@ -1310,47 +197,89 @@ int launch_block_order(const double *dk_coarse, const int nc[3], int nx, int ny,
     return PTV_OK;
 }
 
-static const int kKmaxList[] = {4, 8, 12, 16, 24, 32, 40, 48, 56, 64};
+// list lengths: exact (d2, slot) pair lists serve k <= 12 (length >= k); packed-key lists
+// serve 13 <= k <= 127 (length >= k + 1: the near-tie slot)
+static const int kKmaxExact[] = {4, 8, 12};
+static const int kKmaxKeys[] = {16, 24, 32, 40, 48, 56, 64, 96, 128};
 
 int kmax_for(int k) {
-    for (int km : kKmaxList)
+    if (k < 1) return 0;
+    for (int km : kKmaxExact)
         if (k <= km) return km;
+    for (int km : kKmaxKeys)
+        if (k + 1 <= km) return km;
     return 0;
 }
 
-template <int KMAX, int MODE>
-static void launch_m(dim3 grid, hipStream_t s, const KnnKernelArgs &ka, const Binned &b, const double *ax,
-                     const double *ay, const double *az, const double *qx, const double *qy, const double *qz,
-                     const uint8_t *mask, double *U, double *V, double *W) {
-    if constexpr ((KMAX == 8 || PTV_STAMP_ALL) && MODE != kModeSlots) {
-        // stamps record the main launch, or the lattice-level launches under PTV_STAMP_LATTICE=1
-        const char *sl = std::getenv("PTV_STAMP_LATTICE");
-        const int stamp_mode = (sl && sl[0] == '1') ? kModeKDist : kModeInterp;
-        if (g_dbg != nullptr && MODE == stamp_mode) {
-            hipLaunchKernelGGL((k_knn_interp<KMAX, true, MODE>), grid, dim3(256), 0, s, ka, b.prec, b.pval, b.cstart,
-                               ax, ay, az, qx, qy, qz, mask, U, V, W, g_dbg, g_dbg_cap);
-            return;
-        }
+// the list-length instantiations live in ptv_knn_k*.hip (parallel compilation)
+#define PTV_KNN_EXTERN(K, E)                                                                           \
+    extern template void launch_t<K, E>(dim3, hipStream_t, const KnnKernelArgs &, const Binned &, const double *, \
+                                        const double *, const double *, const double *, const double *,        \
+                                        const double *, const uint8_t *, double *, double *, double *);
+PTV_KNN_EXTERN(4, false)
+PTV_KNN_EXTERN(8, false)
+PTV_KNN_EXTERN(12, false)
+PTV_KNN_EXTERN(16, false)
+PTV_KNN_EXTERN(16, true)
+PTV_KNN_EXTERN(24, false)
+PTV_KNN_EXTERN(24, true)
+PTV_KNN_EXTERN(32, false)
+PTV_KNN_EXTERN(32, true)
+PTV_KNN_EXTERN(40, false)
+PTV_KNN_EXTERN(40, true)
+PTV_KNN_EXTERN(48, false)
+PTV_KNN_EXTERN(48, true)
+PTV_KNN_EXTERN(56, false)
+PTV_KNN_EXTERN(56, true)
+PTV_KNN_EXTERN(64, false)
+PTV_KNN_EXTERN(64, true)
+PTV_KNN_EXTERN(96, false)
+PTV_KNN_EXTERN(96, true)
+PTV_KNN_EXTERN(128, false)
+PTV_KNN_EXTERN(128, true)
+#undef PTV_KNN_EXTERN
+
+static int launch_kmax(int km, bool exact, dim3 grid, hipStream_t s, const KnnKernelArgs &ka, const Binned &b,
+                       const double *ax, const double *ay, const double *az, const double *qx, const double *qy,
+                       const double *qz, const uint8_t *mask, double *U, double *V, double *W) {
+    switch (km) {
+#define PTV_CASE(K)                                                                          \
+    case K:                                                                                  \
+        if constexpr (K >= 16) {                                                             \
+            if (exact) {                                                                     \
+                launch_t<K, true>(grid, s, ka, b, ax, ay, az, qx, qy, qz, mask, U, V, W);    \
+                break;                                                                       \
+            }                                                                                \
+        }                                                                                    \
+        launch_t<K, false>(grid, s, ka, b, ax, ay, az, qx, qy, qz, mask, U, V, W);           \
+        break;
+        PTV_CASE(4)
+        PTV_CASE(8)
+        PTV_CASE(12)
+        PTV_CASE(16)
+        PTV_CASE(24)
+        PTV_CASE(32)
+        PTV_CASE(40)
+        PTV_CASE(48)
+        PTV_CASE(56)
+        PTV_CASE(64)
+        PTV_CASE(96)
+        PTV_CASE(128)
+#undef PTV_CASE
+        default:
+            set_error("no k-NN list of length " + std::to_string(km));
+            return PTV_E_UNSUPPORTED;
     }
-    hipLaunchKernelGGL((k_knn_interp<KMAX, false, MODE>), grid, dim3(256), 0, s, ka, b.prec, b.pval, b.cstart, ax, ay,
-                       az, qx, qy, qz, mask, U, V, W, (unsigned long long *)nullptr, 0LL);
+    PTV_HIP(hipGetLastError());
+    return PTV_OK;
 }
 
-template <int KMAX>
-static void launch_t(dim3 grid, hipStream_t s, const KnnKernelArgs &ka, const Binned &b, const double *ax,
-                     const double *ay, const double *az, const double *qx, const double *qy, const double *qz,
-                     const uint8_t *mask, double *U, double *V, double *W) {
-    switch (ka.mode) {
-        case kModeKDist: launch_m<KMAX, kModeKDist>(grid, s, ka, b, ax, ay, az, qx, qy, qz, mask, U, V, W); break;
-        case kModeSlots: launch_m<KMAX, kModeSlots>(grid, s, ka, b, ax, ay, az, qx, qy, qz, mask, U, V, W); break;
-        case kModeRadius:
-            if constexpr (KMAX == 4) launch_m<KMAX, kModeRadius>(grid, s, ka, b, ax, ay, az, qx, qy, qz, mask, U, V, W);
-            break;
-        case kModeFilter:
-            if constexpr (KMAX >= 4) launch_m<KMAX, kModeFilter>(grid, s, ka, b, ax, ay, az, qx, qy, qz, mask, U, V, W);
-            break;
-        default: launch_m<KMAX, kModeInterp>(grid, s, ka, b, ax, ay, az, qx, qy, qz, mask, U, V, W);
-    }
+static dim3 grid_for(long long nblocks) {
+    // a dispatch holds < 2^32 work-items per dimension: above 2^23 blocks of 256 the grid is
+    // 2-D, x a multiple of 8 so that the linear order still deals blocks round-robin over XCDs
+    constexpr long long kMaxGridX = 1LL << 23;
+    return dim3(nblocks <= kMaxGridX ? (unsigned)nblocks : (unsigned)kMaxGridX,
+                nblocks <= kMaxGridX ? 1u : (unsigned)((nblocks + kMaxGridX - 1) / kMaxGridX));
 }
 
 int launch_knn(const KnnLaunch &a, const Binned &b, const double *ax, const double *ay, const double *az,
@@ -1358,9 +287,10 @@ int launch_knn(const KnnLaunch &a, const Binned &b, const double *ax, const doub
                double *W, hipStream_t s) {
     const int km = a.mode == kModeRadius ? 4 : kmax_for(a.k);
     if (km == 0) {
-        set_error("k=" + std::to_string(a.k) + " exceeds the GPU k-NN list limit (64)");
+        set_error("k=" + std::to_string(a.k) + " exceeds the GPU k-NN list limit (127)");
         return PTV_E_UNSUPPORTED;
     }
+    const bool keys = km >= 16;
     if (a.z1 <= a.z0) return PTV_OK;
     KnnKernelArgs ka;
     ka.cg = a.cg;
@@ -1376,7 +306,7 @@ int launch_knn(const KnnLaunch &a, const Binned &b, const double *ax, const doub
     ka.separable = a.separable;
     ka.method = a.method;
     ka.k = a.k;
-    ka.kpad = km - a.k;
+    ka.kpad = km - a.k - (keys ? 1 : 0);
     ka.power = a.power;
     ka.eps = a.eps;
     ka.flags = a.flags;
@@ -1411,35 +341,51 @@ int launch_knn(const KnnLaunch &a, const Binned &b, const double *ax, const doub
     }
     ka.rall = sqrt(diag2) * (1.0 + 1e-9) + a.cg.mg;
     const long long nblocks = (long long)ka.ntxb * ka.nty * ka.ntz;
-    if (nblocks > 0x7fffffffLL) {
+    if (nblocks > 0x7fffffffLL || (keys && nblocks >= (1LL << 30))) {
         set_error("grid too large for one launch");
         return PTV_E_ARG;
     }
-    // a dispatch holds < 2^32 work-items per dimension: above 2^23 blocks of 256 the grid is
-    // 2-D, x a multiple of 8 so that the linear order still deals blocks round-robin over XCDs
-    constexpr long long kMaxGridX = 1LL << 23;
     ka.nblocks = (int)nblocks;
-    dim3 grid(nblocks <= kMaxGridX ? (unsigned)nblocks : (unsigned)kMaxGridX,
-              nblocks <= kMaxGridX ? 1u : (unsigned)((nblocks + kMaxGridX - 1) / kMaxGridX));
-    switch (km) {
-#define PTV_CASE(K) \
-    case K: launch_t<K>(grid, s, ka, b, ax, ay, az, qx, qy, qz, mask, U, V, W); break;
-        PTV_CASE(4)
-        PTV_CASE(8)
-        PTV_CASE(12)
-        PTV_CASE(16)
-        PTV_CASE(24)
-        PTV_CASE(32)
-        PTV_CASE(40)
-        PTV_CASE(48)
-        PTV_CASE(56)
-        PTV_CASE(64)
-#undef PTV_CASE
-        default:
-            return PTV_E_UNSUPPORTED;
+    // packed keys: slot bits B (the largest slot is n - 1) and the key -> d2 bound factor
+    int B = 1;
+    while (B < 31 && (1LL << B) < b.n) ++B;
+    ka.smask = (uint32_t)((1ULL << B) - 1ULL);
+    ka.kscale = 1.0 + std::ldexp(1.0, B - 51);
+    ka.rep_cnt = nullptr;
+    ka.rep_list = nullptr;
+    ka.rep_cap = 0;
+    ka.tiles = nullptr;
+    ka.ntiles = 0;
+    const bool repair = keys && a.mode != kModeKDist && a.mode != kModeRadius;
+    if (repair) {
+        if (a.rep_cnt == nullptr || a.rep_list == nullptr || a.h_rep == nullptr) {
+            set_error("key-list k-NN launch needs its near-tie repair buffers");
+            return PTV_E_ARG;
+        }
+        ka.rep_cnt = a.rep_cnt;
+        ka.rep_list = a.rep_list;
+        ka.rep_cap = a.rep_cap;
+        PTV_HIP(hipMemsetAsync(a.rep_cnt, 0, sizeof(unsigned int), s));
     }
-    PTV_HIP(hipGetLastError());
-    return PTV_OK;
+    const int rc = launch_kmax(km, false, grid_for(nblocks), s, ka, b, ax, ay, az, qx, qy, qz, mask, U, V, W);
+    if (rc != PTV_OK || !repair) return rc;
+    // near-tie repair: the listed tiles again with the exact (d2, slot) pair lists
+    PTV_HIP(hipMemcpyAsync(a.h_rep, a.rep_cnt, sizeof(unsigned int), hipMemcpyDeviceToHost, s));
+    PTV_HIP(hipStreamSynchronize(s));
+    const unsigned int nrep = *a.h_rep;
+    if (a.n_repair != nullptr) *a.n_repair += nrep;
+    if (nrep == 0) return PTV_OK;
+    KnnKernelArgs kr = ka;
+    kr.kpad = km - a.k;
+    kr.rep_cnt = nullptr;
+    if ((long long)nrep <= (long long)a.rep_cap) {
+        kr.tiles = a.rep_list;
+        kr.ntiles = (int)nrep;
+        kr.nblocks = (int)((nrep + 3) / 4);
+        return launch_kmax(km, true, grid_for(kr.nblocks), s, kr, b, ax, ay, az, qx, qy, qz, mask, U, V, W);
+    }
+    // more than the list holds: the whole launch again
+    return launch_kmax(km, true, grid_for(nblocks), s, kr, b, ax, ay, az, qx, qy, qz, mask, U, V, W);
 }
 
 }  // namespace ptv

@@ -1,0 +1,16 @@
+// ptv_knn_kb.hip — k-NN kernel instantiations for list lengths 12, 16
+// (split from ptv_knn.hip so that the list lengths compile in parallel)
+#include "ptv_knn_impl.hpp"
+
+namespace ptv {
+
+#define PTV_KNN_INST(K, E)                                                                      \
+    template void launch_t<K, E>(dim3, hipStream_t, const KnnKernelArgs &, const Binned &, const double *, \
+                                 const double *, const double *, const double *, const double *,        \
+                                 const double *, const uint8_t *, double *, double *, double *);
+PTV_KNN_INST(12, false)
+PTV_KNN_INST(16, false)
+PTV_KNN_INST(16, true)
+#undef PTV_KNN_INST
+
+}  // namespace ptv

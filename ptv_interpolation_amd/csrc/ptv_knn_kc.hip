@@ -1,0 +1,17 @@
+// ptv_knn_kc.hip — k-NN kernel instantiations for list lengths 24, 32
+// (split from ptv_knn.hip so that the list lengths compile in parallel)
+#include "ptv_knn_impl.hpp"
+
+namespace ptv {
+
+#define PTV_KNN_INST(K, E)                                                                      \
+    template void launch_t<K, E>(dim3, hipStream_t, const KnnKernelArgs &, const Binned &, const double *, \
+                                 const double *, const double *, const double *, const double *,        \
+                                 const double *, const uint8_t *, double *, double *, double *);
+PTV_KNN_INST(24, false)
+PTV_KNN_INST(24, true)
+PTV_KNN_INST(32, false)
+PTV_KNN_INST(32, true)
+#undef PTV_KNN_INST
+
+}  // namespace ptv

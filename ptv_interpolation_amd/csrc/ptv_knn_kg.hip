@@ -1,0 +1,15 @@
+// ptv_knn_kg.hip — k-NN kernel instantiations for list lengths 96
+// (split from ptv_knn.hip so that the list lengths compile in parallel)
+#include "ptv_knn_impl.hpp"
+
+namespace ptv {
+
+#define PTV_KNN_INST(K, E)                                                                      \
+    template void launch_t<K, E>(dim3, hipStream_t, const KnnKernelArgs &, const Binned &, const double *, \
+                                 const double *, const double *, const double *, const double *,        \
+                                 const double *, const uint8_t *, double *, double *, double *);
+PTV_KNN_INST(96, false)
+PTV_KNN_INST(96, true)
+#undef PTV_KNN_INST
+
+}  // namespace ptv
