@@ -61,6 +61,9 @@ extern "C" {
  * the fused `U.astype(np.float32)` of main.py:230, applied after the float64 result, the
  * nan_to_num and the mask (half the output bytes).  Arithmetic stays float64. */
 #define PTV_FLAG_OUT_F32 2u
+/* local RBF, diagnostics: SPD systems through the LDS-broadcast kernel (k_rbf_spd, the one the
+ * register kernel's out-of-range-pivot rerun uses) instead of k_rbf_spd16 (ABI v8) */
+#define PTV_FLAG_RBF_SPD_LDS 4u
 
 typedef struct ptv_ctx ptv_ctx;
 

@@ -83,6 +83,7 @@ class LinearParams(C.Structure):
 F64 = 0
 F32 = 1
 FLAG_OUT_F32 = 2  # U, V, W written as float32 (main.py:230 astype, fused)
+FLAG_RBF_SPD_LDS = 4  # local RBF diagnostics: SPD systems through the LDS-broadcast kernel
 
 
 class DivParams(C.Structure):

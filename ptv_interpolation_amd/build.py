@@ -37,6 +37,7 @@ TAG = os.environ.get("PTV_BUILD_TAG", "")
 if TAG:
     LIB = os.path.join(os.path.dirname(HERE), "ab", f"libptv_{TAG}.so")
     BUILD = os.path.join(HERE, "csrc", "_build_" + TAG)
+    EXTRA_FLAGS.append("-DPTV_DEV_KNOBS=1")  # only dev builds read the PTV_* tuning variables
 
 
 def hipcc() -> str:

@@ -350,7 +350,7 @@ CellGrid make_cell_grid(const double lo_in[3], const double hi_in[3], int64_t n,
         maxabs = std::max(maxabs, std::max(std::fabs(lo_in[a]), std::fabs(hi_in[a])));
     }
     if (!(occ > 0.0)) occ = kDefaultOccupancy;
-    if (const char *e = std::getenv("PTV_CELL_OCC")) occ = std::atof(e);  // dev override
+    if (const char *e = dev_knob("PTV_CELL_OCC")) occ = std::atof(e);  // dev override
     double vol = 1.0;
     int dims = 0;
     for (int a = 0; a < 3; ++a)
@@ -364,7 +364,7 @@ CellGrid make_cell_grid(const double lo_in[3], const double hi_in[3], int64_t n,
     // length, so thin x-cells trim the runs' ends (fewer candidates outside the sub-balls)
     // without adding rows.
     double xref = std::max(1.0, xref_in);
-    if (const char *e = std::getenv("PTV_CELL_XREF")) xref = std::max(1.0, std::atof(e));  // dev override
+    if (const char *e = dev_knob("PTV_CELL_XREF")) xref = std::max(1.0, std::atof(e));  // dev override
     for (int iter = 0; iter < 64; ++iter) {  // cap the cell count (memory) by growing cs
         long long tot = 1;
         for (int a = 0; a < 3; ++a) {
@@ -491,7 +491,7 @@ int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchP
         while (nlat < kMaxLattice) {
             const long long pts = (long long)n[0] * n[1] * n[2];
             long long stop = kLatticeStopPoints;
-            if (const char *e = std::getenv("PTV_LAT_STOP")) stop = std::atoll(e);  // dev override
+            if (const char *e = dev_knob("PTV_LAT_STOP")) stop = std::atoll(e);  // dev override
             if (pts <= stop || std::min(n[0], std::min(n[1], n[2])) < 9) break;
             Lat &L = lat[nlat];
             for (int d = 0; d < 3; ++d) L.n[d] = n[d] <= 1 ? 1 : (n[d] - 1 + kLatticeStep - 1) / kLatticeStep + 1;
@@ -541,7 +541,7 @@ int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchP
             lat[l].recs = c->lat_recs[l].p;
         }
         KnnLaunch ll = kl;
-        const char *no_order = std::getenv("PTV_NO_LAT_ORDER");  // dev knob: 1 = XCD-contiguous order
+        const char *no_order = dev_knob("PTV_NO_LAT_ORDER");  // dev knob: 1 = XCD-contiguous order
         if (!(no_order && no_order[0] == '1')) {
             const long long nb = (long long)(((lat[l].n[0] + 3) / 4 + 3) / 4) * ((lat[l].n[1] + 3) / 4) *
                                  ((lat[l].n[2] + 3) / 4);
@@ -563,7 +563,7 @@ int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchP
         ll.cb.az = lat[l + 1].az;
         ll.cb.dk = lat[l + 1].dk;
         ll.cb.recs = lat[l + 1].recs;
-        if (const char *e = std::getenv("PTV_LAT_SEEDS"))  // dev knob: 0 = lattice levels unseeded
+        if (const char *e = dev_knob("PTV_LAT_SEEDS"))  // dev knob: 0 = lattice levels unseeded
             if (e[0] == '0') ll.cb.recs = nullptr;
         for (int d = 0; d < 3; ++d) ll.cb.n[d] = lat[l + 1].n[d];
         PTV_TRY(launch_knn(ll, b, lat[l].ax, lat[l].ay, lat[l].az, nullptr, nullptr, nullptr, nullptr, lat[l].dk,
@@ -614,7 +614,7 @@ bool lattice_built(const ptv_grid *g, int lattice_bounds) {
     if (lattice_bounds < 0) return false;
     const long long n[3] = {g->nx, g->ny, g->z_end - g->z_begin};
     long long stop = kLatticeStopPoints;
-    if (const char *e = std::getenv("PTV_LAT_STOP")) stop = std::atoll(e);
+    if (const char *e = dev_knob("PTV_LAT_STOP")) stop = std::atoll(e);
     return n[0] * n[1] * n[2] > stop && std::min(n[0], std::min(n[1], n[2])) >= 9;
 }
 
@@ -1306,7 +1306,7 @@ int ptv_debug_stamps(ptv_ctx *c, int mode, double *out) {
         PTV_HIP(hipDeviceSynchronize());
         std::vector<unsigned long long> h((size_t)cap * nf);
         PTV_HIP(hipMemcpy(h.data(), c->dbg.p, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-        if (const char *dump = std::getenv("PTV_STAMPS_DUMP")) {  // raw per-wave records (dev tool)
+        if (const char *dump = dev_knob("PTV_STAMPS_DUMP")) {  // raw per-wave records (dev tool)
             if (FILE *f = std::fopen(dump, "wb")) {
                 std::fwrite(h.data(), sizeof(unsigned long long), h.size(), f);
                 std::fclose(f);
@@ -1585,8 +1585,8 @@ int run_filter(ptv_ctx *c, const ptv_particles *p, const ptv_filter_params *prm,
     g.z_begin = 0;
     g.z_end = g.nz;
     double r0s = 0.0, occ = 0.0;
-    if (const char *e = std::getenv("PTV_FILTER_R0")) r0s = std::atof(e);       // dev knobs
-    if (const char *e = std::getenv("PTV_FILTER_OCC")) occ = std::atof(e);
+    if (const char *e = dev_knob("PTV_FILTER_R0")) r0s = std::atof(e);       // dev knobs
+    if (const char *e = dev_knob("PTV_FILTER_OCC")) occ = std::atof(e);
     const SearchParams sp{PTV_METHOD_IDW, prm->k + 1, 2.0, 1e-10, 0u, occ, r0s, -1};
     KnnLaunch kl;
     Binned b{};

@@ -4,9 +4,22 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
 #include <string>
 
 namespace ptv {
+
+// Dev tuning knobs (environment variables) are read only by builds compiled with
+// -DPTV_DEV_KNOBS=1 (the tools/ A/B and stamp builds); the shipped library never lets the
+// environment change its kernels or launch shapes.
+inline const char *dev_knob(const char *name) {
+#if defined(PTV_DEV_KNOBS) && PTV_DEV_KNOBS
+    return std::getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
 
 // ---------------------------------------------------------------------------
 // Error plumbing: thread-local message + negative codes (include/ptv_api.h).

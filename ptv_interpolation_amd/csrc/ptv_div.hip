@@ -221,7 +221,7 @@ int launch_divergence(const DivArgs &a, const void *U, const void *V, const void
                       hipStream_t s) {
     if (a.z_end <= a.z_begin) return PTV_OK;
     DivArgs b = a;
-    if (const char *e = std::getenv("PTV_DIV_XCD")) b.xcd = std::atoi(e);  // dev knob
+    if (const char *e = dev_knob("PTV_DIV_XCD")) b.xcd = std::atoi(e);  // dev knob
     return launch_typed(b, U, V, W, M, out, s);
 }
 

@@ -329,7 +329,7 @@ int launch_knn(const KnnLaunch &a, const Binned &b, const double *ax, const doub
     }
     ka.order = a.order;
     ka.seed_n = a.k;
-    if (const char *e = std::getenv("PTV_SEED_N")) ka.seed_n = std::max(1, std::min(a.k, std::atoi(e)));  // dev knob
+    if (const char *e = dev_knob("PTV_SEED_N")) ka.seed_n = std::max(1, std::min(a.k, std::atoi(e)));  // dev knob
     if (a.mode == kModeSlots && (a.slots == nullptr || (a.z0 - ka.lz0) % 4 != 0)) {
         set_error("slot-mode k-NN launch needs an output buffer and a tile-aligned first plane");
         return PTV_E_ARG;

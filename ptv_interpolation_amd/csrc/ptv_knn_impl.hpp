@@ -62,6 +62,10 @@ namespace ptv {
 #define PTV_KNN_WAVES_MID 3  // 8 < KMAX <= 32: capped for 3 waves per SIMD (Sibson k=30 and the RBF k=32 slot search -7 %)
 #endif
 
+#ifndef PTV_KNN_KEYI_2W
+#define PTV_KNN_KEYI_2W 40  // key-list interpolation kernels of at least this many slots: 2 waves per SIMD
+#endif
+
 #ifndef PTV_STAMP_ALL
 #define PTV_STAMP_ALL 0  // dev builds: 1 = the STAMP instantiation for every KMAX (not only 8)
 #endif
@@ -428,16 +432,18 @@ __device__ __forceinline__ double axis_gap(int c, double o, double cs, double lo
 template <int KMAX, bool EXACT>
 constexpr bool kKeyList = KMAX >= 16 && !EXACT;
 
-template <int KMAX, bool EXACT>
+template <int KMAX, int MODE, bool EXACT>
 constexpr int knn_waves() {
     if (KMAX <= 4) return PTV_KNN_WAVES_SMALL;
     if (KMAX <= 8) return PTV_KNN_WAVES;
-    if (kKeyList<KMAX, EXACT>) return KMAX <= 32 ? PTV_KNN_WAVES_MID : (KMAX <= 64 ? PTV_KNN_WAVES_BIG : 1);
+    // key lists: the search fits 3 waves per SIMD up to 32 slots, the streamed interpolation
+    // epilogue (slots + two blocks of records + three pairwise accumulators) needs 2 from 24
+    if (kKeyList<KMAX, EXACT> && MODE == kModeInterp && KMAX >= PTV_KNN_KEYI_2W) return KMAX <= 64 ? 2 : 1;
     return KMAX <= 32 ? PTV_KNN_WAVES_MID : (KMAX <= 64 ? PTV_KNN_WAVES_BIG : 1);
 }
 
 template <int KMAX, bool STAMP, int MODE, bool EXACT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<KMAX, EXACT>()))) void k_knn_interp(KnnKernelArgs a, const double4 *__restrict__ prec,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<KMAX, MODE, EXACT>()))) void k_knn_interp(KnnKernelArgs a, const double4 *__restrict__ prec,
                                                     const double4 *__restrict__ pval,
                                                     const uint32_t *__restrict__ cstart,
                                                     const double *__restrict__ ax, const double *__restrict__ ay,
@@ -965,7 +971,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                 };
                 uint32_t next_slot = total > 0 ? window_slot(0) : 0u;
                 double4 next_rec = prec[next_slot];
-                for (int src = 0; src < total; src += 64) {
+                // the pass's last round runs at least one (possibly empty) window, so that the
+                // final flush below is the loop's own (one inlined copy of the insert network)
+                const bool last_round = rb + 64 * kRowsPerLane >= nrows;
+                const int tot_it = (total == 0 && last_round) ? 1 : total;
+                for (int src = 0; src < tot_it; src += 64) {
                     const uint32_t slot = next_slot;
                     const double4 p4 = next_rec;
                     if (src + 64 < total) {
@@ -1004,10 +1014,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                     nbuf += __builtin_popcountll(km);
                     n_cand += (uint32_t)min(64, total - src);
                     stamp(t_copy);
-                    if (nbuf > kCap - 64) flush();
+                    if (nbuf > kCap - 64 || (last_round && src + 64 >= tot_it)) flush();
                 }
             }
-            flush();
             // ---- exactness: lanes with k-th distance <= R are final ----
             // (key lists: the key bound covers every candidate sharing the k-th key's truncation,
             // so the (k+1)-th slot sees them all too)
@@ -1228,7 +1237,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
         store_out(a.flags, U, V, W, vo, o[0], o[1], o[2]);
         return;
     }
-    if constexpr (KSL && MODE == kModeInterp) {
+    if constexpr (KSL && MODE == kModeInterp && KMAX <= 32) {
+        // up to 32 slots: blocks unrolled at compile time (the loads of different blocks overlap,
+        // measured faster than the rolled loop below at 3 waves per SIMD: Sibson k = 30 79 vs 92 ms)
         // Key lists (k >= 13): the weights are streamed in blocks of 8 neighbours from the exact
         // d2, recomputed from the records (the keys hold truncated d2), in the reference's order:
         // interpolator.py:142-153 (IDW), :102-122 (Sibson).  Register-kept distances where the
@@ -1418,6 +1429,221 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
         store_out(a.flags, U, V, W, vo, out[0], out[1], out[2]);
         write_stamps();
         return;
+    } else if constexpr (KSL && MODE == kModeInterp) {
+        // Key lists (k >= 13): the weights are streamed in blocks of 8 neighbours from the exact
+        // d2, recomputed from the records (the keys hold truncated d2), in the reference's order:
+        // interpolator.py:142-153 (IDW), :102-122 (Sibson).  Every pass is a rolled loop over the
+        // blocks (a fully unrolled epilogue was tens of KB of straight-line code per wave): block
+        // b takes slots 0..7 of a copy of the slot list that is rotated down by 8 per block.
+        const int k = a.k;
+        // ksl rotates circularly by 8 per block; rewind() completes the turn after a pass
+        int rot = 0;  // blocks rotated so far (mod KMAX / 8)
+        auto rotate8 = [&]() {
+            int t[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) t[i] = ksl[i];
+#pragma unroll
+            for (int j = 0; j + 8 < KMAX; ++j) ksl[j] = ksl[j + 8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) ksl[KMAX - 8 + i] = t[i];
+        };
+        auto rewind = [&]() {
+#pragma unroll 1
+            for (; rot != 0 && rot < KMAX / 8; ++rot) rotate8();
+            rot = 0;
+        };
+        auto next_slots = [&](int m, int (&s8)[8]) {
+            const int s0 = ksl[0];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) s8[i] = m + i < k ? ksl[i] : s0;
+            rotate8();
+            ++rot;
+        };
+        // x, y, z of 8 records (24 of each 32-byte record: 48 VGPRs in flight, not 64)
+        auto xyz_block = [&](const double4 *__restrict__ src, const int (&s8)[8], double (&x)[8], double (&y)[8],
+                             double (&z)[8]) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const double *r = reinterpret_cast<const double *>(src + s8[i]);
+                const double2 xy = *reinterpret_cast<const double2 *>(r);
+                x[i] = xy.x;
+                y[i] = xy.y;
+                z[i] = r[2];
+            }
+        };
+        auto d2_block = [&](const int (&s8)[8], double (&d2)[8]) {
+            double x[8], y[8], z[8];
+            xyz_block(prec, s8, x, y, z);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const double dx = qx - x[i], dy = qy - y[i], dz = qz - z[i];
+                d2[i] = (dx * dx + dy * dy) + dz * dz;
+            }
+        };
+        double out[3];
+        bool ok = true;
+        double prev = -1.0;
+        if (a.method == PTV_METHOD_SIBSON) {
+            // pass 1: d, 1/(d + eps) -> sum (pairwise), sum d -> mean; the order check
+            PairwiseStream ps_inv, ps_d;
+            rewind();
+#pragma unroll 1
+            for (int m = 0; m < k; m += 8) {
+                int s8[8];
+                next_slots(m, s8);
+                double d2[8], dv[8], iv[8];
+                d2_block(s8, d2);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    if (m + i < k) {
+                        ok = ok && !(d2[i] < prev);
+                        prev = d2[i];
+                    }
+                    dv[i] = sqrt_cr(d2[i]);
+                    iv[i] = 1.0 / (dv[i] + a.eps);
+                }
+                ps_inv.add(m, k, iv);
+                ps_d.add(m, k, dv);
+            }
+            stamp(t_seed);  // stamp builds: pass 1 of the key-list epilogue (no seeds above 8 slots)
+            if (__builtin_amdgcn_ballot_w64(amb || !ok) != 0) {
+                list_tile();
+                return;
+            }
+            const double s_inv = ps_inv.finish(k);
+            const double mean = ps_d.finish(k) / (double)k;
+            // pass 2: std (ddof 0)
+            PairwiseStream ps_var;
+            rewind();
+#pragma unroll 1
+            for (int m = 0; m < k; m += 8) {
+                int s8[8];
+                next_slots(m, s8);
+                double d2[8], t[8];
+                d2_block(s8, d2);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const double c = sqrt_cr(d2[i]) - mean;
+                    t[i] = c * c;
+                }
+                ps_var.add(m, k, t);
+            }
+            const double den = sqrt(ps_var.finish(k) / (double)k) + a.eps;
+            auto w_of = [&](double d2) {
+                const double d = sqrt_cr(d2);
+                return (1.0 / (d + a.eps)) / s_inv * exp(-d / den);
+            };
+            // pass 3: the exponential weights' sum
+            PairwiseStream ps_w;
+            rewind();
+#pragma unroll 1
+            for (int m = 0; m < k; m += 8) {
+                int s8[8];
+                next_slots(m, s8);
+                double d2[8], w[8];
+                d2_block(s8, d2);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) w[i] = w_of(d2[i]);
+                ps_w.add(m, k, w);
+            }
+            const double s2 = ps_w.finish(k);
+            // pass 4: normalised weights times the values
+            PairwiseStream pu, pv, pw;
+            rewind();
+#pragma unroll 1
+            for (int m = 0; m < k; m += 8) {
+                int s8[8];
+                next_slots(m, s8);
+                double d2[8], wn[8];
+                d2_block(s8, d2);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) wn[i] = w_of(d2[i]) / s2;
+                double tu[8], tv[8], tw8[8];
+                xyz_block(pval, s8, tu, tv, tw8);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    tu[i] = wn[i] * tu[i];
+                    tv[i] = wn[i] * tv[i];
+                    tw8[i] = wn[i] * tw8[i];
+                }
+                pu.add(m, k, tu);
+                pv.add(m, k, tv);
+                pw.add(m, k, tw8);
+            }
+            out[0] = pu.finish(k);
+            out[1] = pv.finish(k);
+            out[2] = pw.finish(k);
+        } else {
+            // pass 1: w = 1/(d**p + eps) -> sum (pairwise); the order check
+            auto w_of = [&](double d2) { return 1.0 / (np_pow(sqrt_cr(d2), a.power) + a.eps); };
+            PairwiseStream ps;
+            double wmin = INFINITY;
+            rewind();
+#pragma unroll 1
+            for (int m = 0; m < k; m += 8) {
+                int s8[8];
+                next_slots(m, s8);
+                double d2[8], w[8];
+                d2_block(s8, d2);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    if (m + i < k) {
+                        ok = ok && !(d2[i] < prev);
+                        prev = d2[i];
+                    }
+                    w[i] = w_of(d2[i]);
+                    if (m + i < k) wmin = fmin(wmin, w[i]);
+                }
+                ps.add(m, k, w);
+            }
+            stamp(t_seed);  // stamp builds: pass 1 of the key-list epilogue (no seeds above 8 slots)
+            if (__builtin_amdgcn_ballot_w64(amb || !ok) != 0) {
+                list_tile();
+                return;
+            }
+            const double s = ps.finish(k);
+            // w_j / s through one reciprocal when every quotient is normal (see the k <= 12 path)
+            const bool fast = __builtin_amdgcn_ballot_w64(!(s <= 0x1p1000 && wmin >= s * 0x1p-1000)) == 0;
+            const double rs = 1.0 / s;
+            // pass 2: normalised weights times the values
+            PairwiseStream pu, pv, pw;
+            rewind();
+#pragma unroll 1
+            for (int m = 0; m < k; m += 8) {
+                int s8[8];
+                next_slots(m, s8);
+                double d2[8], wn[8];
+                d2_block(s8, d2);
+                if (fast) {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) wn[i] = div_by(w_of(d2[i]), s, rs);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) wn[i] = w_of(d2[i]) / s;
+                }
+                double tu[8], tv[8], tw8[8];
+                xyz_block(pval, s8, tu, tv, tw8);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    tu[i] = wn[i] * tu[i];
+                    tv[i] = wn[i] * tv[i];
+                    tw8[i] = wn[i] * tw8[i];
+                }
+                pu.add(m, k, tu);
+                pv.add(m, k, tv);
+                pw.add(m, k, tw8);
+            }
+            out[0] = pu.finish(k);
+            out[1] = pv.finish(k);
+            out[2] = pw.finish(k);
+        }
+        if (a.flags & PTV_FLAG_NAN_TO_NUM) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) out[c] = nan_to_num(out[c]);
+        }
+        store_out(a.flags, U, V, W, vo, out[0], out[1], out[2]);
+        write_stamps();
+        return;
     } else if constexpr (!KEYS) {
 
     // left-shift the list by kpad so real entries occupy slots 0..k-1 (kpad uniform)
@@ -1532,7 +1758,7 @@ void launch_m(dim3 grid, hipStream_t s, const KnnKernelArgs &ka, const Binned &b
                      const uint8_t *mask, double *U, double *V, double *W) {
     if constexpr ((KMAX == 8 || PTV_STAMP_ALL) && MODE != kModeSlots && !EXACT) {
         // stamps record the main launch, or the lattice-level launches under PTV_STAMP_LATTICE=1
-        const char *sl = std::getenv("PTV_STAMP_LATTICE");
+        const char *sl = dev_knob("PTV_STAMP_LATTICE");
         const int stamp_mode = (sl && sl[0] == '1') ? kModeKDist : kModeInterp;
         if (g_dbg != nullptr && MODE == stamp_mode) {
             hipLaunchKernelGGL((k_knn_interp<KMAX, true, MODE, false>), grid, dim3(256), 0, s, ka, b.prec, b.pval,

@@ -1062,7 +1062,7 @@ static void launch_spd_m(const RbfKernelArgs &ka, long long nvox, hipStream_t s,
 
 // whether the system is symmetric positive definite (see k_rbf_spd) and of a size it serves
 static bool rbf_spd(const RbfKernelArgs &ka, const double *smooth) {
-    if (const char *e = std::getenv("PTV_RBF_SPD"))  // dev knob: 0 = always the pivoting kernel
+    if (const char *e = dev_knob("PTV_RBF_SPD"))  // dev knob: 0 = always the pivoting kernel
         if (e[0] == '0') return false;  // (1 = the LDS-broadcast SPD kernel, see launch_rbf)
     const bool pd_kernel = ka.kernel == PTV_RBF_GAUSSIAN || ka.kernel == PTV_RBF_INVERSE_MULTIQUADRIC ||
                            ka.kernel == PTV_RBF_INVERSE_QUADRATIC;
@@ -1104,8 +1104,8 @@ int launch_rbf(const RbfKernelArgs &ka, const Binned &b, const uint32_t *slots, 
         return PTV_E_ARG;
     }
     if (rbf_spd(ka, smooth)) {
-        const char *e = std::getenv("PTV_RBF_SPD");  // dev knob: 1 = the LDS-broadcast SPD kernel
-        if (!(e && e[0] == '1') && !ka.spd_lds) {
+        const char *e = dev_knob("PTV_RBF_SPD");  // dev knob: 1 = the LDS-broadcast SPD kernel
+        if (!(e && e[0] == '1') && !ka.spd_lds && !(ka.flags & PTV_FLAG_RBF_SPD_LDS)) {
             const long long waves = (nvox + 3) / 4;
             const dim3 grid((unsigned)((waves + 3) / 4));
 #define PTV_S16(MM, KK) hipLaunchKernelGGL((k_rbf_spd16<MM, KK>), grid, dim3(256), 0, s, ka, b.prec, b.pval, slots, ax, ay, az, qx, qy, qz, mask, U, V, W, status)

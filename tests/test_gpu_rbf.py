@@ -268,15 +268,16 @@ def test_spd_register_kernel_rerun_matches_lds_kernel(ctx, monkeypatch):
     pivots.  Both kernels eliminate in the same order with the same reciprocals wherever the
     fast one serves; their evaluation sums differ in order (16-lane rows of two entries vs a
     32-lane segment sum), so on these ill-conditioned systems they agree to TOL_ILL (checked on
-    a normal case with PTV_RBF_SPD=1 forcing the LDS kernel), and the rerun matches the oracle."""
+    a normal case with PTV_FLAG_RBF_SPD_LDS forcing the LDS kernel), and the rerun matches the oracle."""
     from oracle import cpu_ref
+    from ptv_interpolation_amd import _lib
     from ptv_interpolation_amd.rbf import LocalRBFInterpolator
 
     P, Q, ax = _rand_case(63, 4000, 12)
     fast = LocalRBFInterpolator(P, Q, neighbors=32, kernel="gaussian", epsilon=0.3, degree=-1).evaluate_grid(ax, ax, ax)
-    monkeypatch.setenv("PTV_RBF_SPD", "1")
-    lds = LocalRBFInterpolator(P, Q, neighbors=32, kernel="gaussian", epsilon=0.3, degree=-1).evaluate_grid(ax, ax, ax)
-    monkeypatch.delenv("PTV_RBF_SPD")
+    lds = LocalRBFInterpolator(P, Q, neighbors=32, kernel="gaussian", epsilon=0.3, degree=-1).evaluate_grid(
+        ax, ax, ax, flags=_lib.FLAG_RBF_SPD_LDS)
+    assert any(not np.array_equal(a, b) for a, b in zip(fast, lds))  # two different kernels ran
     for a, b in zip(fast, lds):
         assert normwise(a, b) <= TOL_ILL
     big = LocalRBFInterpolator(P, Q, neighbors=32, kernel="gaussian", epsilon=0.3, degree=-1,
