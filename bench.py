@@ -219,20 +219,40 @@ def row_traffic(*keys):
         return None
 
 
+def lib_sha256():
+    """First 16 hex digits of the loaded library's SHA-256 (tools/traffic.py records the same)."""
+    import hashlib
+
+    from ptv_interpolation_amd import _lib
+
+    try:
+        with open(_lib.LIB_PATH, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
 def traffic_from_profiles():
-    """HBM bytes per main k-NN launch at the headline from the newest profiles/traffic_rNN.json."""
+    """(HBM bytes per main k-NN launch at the headline, its source) from the newest
+    profiles/traffic_rNN.json: PMC counters cannot be collected inside the timed process
+    (rocprofv3 wraps it), so the line cites the profile run and whether it profiled this very
+    library (same SHA-256) or an earlier build."""
     import re
 
-    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "traffic_r*.json"))
-                   if re.fullmatch(r"traffic_r\d+\.json", os.path.basename(f)))  # not traffic_rows_*
+    files = sorted((f for f in glob.glob(os.path.join(ROOT, "profiles", "traffic_r*.json"))
+                    if re.fullmatch(r"traffic_r\d+[a-z]?\.json", os.path.basename(f))),  # not traffic_rows_*
+                   key=os.path.getmtime)
     if not files:
-        return None
+        return None, None
     try:
         with open(files[-1]) as f:
             t = json.load(f)
-        return float(t["hbm_bytes_per_launch"])
+        sha = t.get("lib_sha256")
+        src = {"file": os.path.relpath(files[-1], ROOT), "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes",
+               "lib_sha256": sha, "this_build": sha is not None and sha == lib_sha256()}
+        return float(t["hbm_bytes_per_launch"]), src
     except Exception:
-        return None
+        return None, None
 
 
 def _cpu_line(value, unit, workers, sample, dt):
@@ -245,7 +265,8 @@ def cpu_baseline(args, P, Q, ax, az, z0_grid):
     from oracle import cpu_ref
 
     big = args.particles > 20_000_000
-    planes = min(args.cpu_sample_planes or (4 if big else 16), len(az))
+    # a bounded sample (10-30 s of CPU work): fewer planes for 50M particles or k >= 30
+    planes = min(args.cpu_sample_planes or (4 if big or args.k >= 30 else 16), len(az))
     workers = max(1, min(args.cpu_workers or (4 if big else 16), os.cpu_count() or 1))
     z0 = z0_grid + len(az) // 2 - planes // 2
     t = time.perf_counter()
@@ -666,7 +687,8 @@ def main_interp(args):
         headline_shape = (G == 512 and args.particles == 5_000_000 and k == 8 and not args.mask and not out_f32)
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBPS, 4),
-                "traffic": traffic_from_profiles() if headline_shape else None,
+                "traffic": traffic_from_profiles()[0] if headline_shape else None,
+                "traffic_source": traffic_from_profiles()[1] if headline_shape else None,
                 "kernel": "k_knn_interp<4, radius>" if radius else f"k_knn_interp<{kmax_for(k)}>",
                 "alg_bytes_per_launch": alg,
                 "kernel_ms": round(avg["ms_knn"], 3),

@@ -135,7 +135,7 @@ typedef struct {
     int k;                /* rbf_neighbors, 1 <= k <= n */
     int kernel;           /* PTV_RBF_* */
     double epsilon;       /* shape parameter */
-    int degree;           /* polynomial degree, -1 = no polynomial; k + C(degree+3, 3) <= 64 */
+    int degree;           /* polynomial degree, -1 = no polynomial; k + C(degree+3, 3) <= 128 */
     double smoothing;     /* scalar smoothing, used when smoothing_per_point is NULL */
     const double *smoothing_per_point; /* optional (n,) array, same memory space as the particles */
     const uint8_t *fluid_mask;        /* as ptv_knn_params.fluid_mask */

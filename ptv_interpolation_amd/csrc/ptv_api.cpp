@@ -279,6 +279,7 @@ constexpr double kDefaultOccupancy = 1.2;
 constexpr double kDefaultR0Scale = 1.0;     // first gather radius / expected k-NN radius
 constexpr long long kMaxCells = 1LL << 28;
 constexpr long long kLatticeStopPoints = 50000; // no coarser lattice below this many points
+constexpr size_t kSeedBytesMax = 40ULL << 30;    // lattice seed records per level (C5 2048^3, k = 8: 17 GB)
 
 int validate(const ptv_particles *p, const ptv_grid *g, const void *prm) {
     if (!p || !g || !prm) {
@@ -481,7 +482,7 @@ int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchP
     struct Lat {
         int n[3];
         double *ax, *ay, *az, *dk;
-        float4 *recs;   // NULL on the coarsest (count-bound) level and for k > 8
+        float4 *recs;   // NULL on the coarsest (count-bound) level and past kSeedBytesMax
     };
     Lat lat[kMaxLattice];
     int nlat = 0;
@@ -536,8 +537,11 @@ int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchP
                                        lat[l].n[2], prm->k, kl.r0, lat[l].dk, s));
             continue;
         }
-        if (kmax_for(prm->k) <= 8) {  // seeds are used by the k <= 8 kernels only
-            PTV_TRY(c->lat_recs[l].ensure((size_t)lat[l].n[0] * lat[l].n[1] * lat[l].n[2] * prm->k));
+        // seed records (each lattice point's k-NN, 16 B each) for the next finer level's tiles,
+        // unless they would take more than kSeedBytesMax (then the D(c) + |v - c| bound alone)
+        const size_t nrec = (size_t)lat[l].n[0] * lat[l].n[1] * lat[l].n[2] * prm->k;
+        if (nrec * sizeof(float4) <= kSeedBytesMax) {
+            PTV_TRY(c->lat_recs[l].ensure(nrec));
             lat[l].recs = c->lat_recs[l].p;
         }
         KnnLaunch ll = kl;

@@ -163,7 +163,7 @@ int launch_linear_brute(const LinearKernelArgs &a, int nflag, const double *ax, 
                         hipStream_t s);
 
 // ---- local RBF (ptv_rbf.hip) ----
-constexpr int kRbfMaxSystem = 64;  // k + #monomials per voxel system
+constexpr int kRbfMaxSystem = 128;  // k + #monomials per voxel system (> 64: k_rbf_big, LDS-resident)
 
 struct RbfKernelArgs {
     int nx, ny;      // grid plane

@@ -559,8 +559,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
     };
     // With seed records the seeds' bound is the tighter one for (nearly) every lane: the
     // D(c) + |v - c| bound is then formed only when some active lane got no seed bound.
-    bool seeds_defer = false;
-    if constexpr (KMAX <= 8) seeds_defer = a.cb.recs != nullptr;
+    const bool seeds_defer = a.cb.recs != nullptr;
     double ub = seeds_defer ? INFINITY : lattice_ub();
     // candidates at or beyond the bound can never be among the k nearest
     double ub2 = !active ? -1.0 : (ub < INFINITY ? ub * ub : INFINITY);
@@ -689,6 +688,140 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                 if (__builtin_amdgcn_ballot_w64(active && !(kth < INFINITY)) != 0) {
                     // rare (fewer than k distinct seeds survived the hash): the lattice bound
                     const double u = lattice_ub();
+                    if (u < ub) {
+                        ub = u;
+                        ub2 = u * u;
+                    }
+                }
+                seeded = true;
+                thr = dmin(kth2(), ub2);
+                wave_lds_sync();  // the gather reuses the candidate buffers
+                stamp(t_seed);
+            }
+        }
+        if constexpr (KMAX > 8) {
+            if (a.cb.recs != nullptr) {
+                // ---- seeds (k > 8): the union of the 8 corners' k-NN lists bounds every voxel's
+                //      k-th distance (measured: within 0.03 % of it in volume, the D(c) + |v - c|
+                //      bound 2.2x).  8 rounds of up to 64 records (one corner per round),
+                //      deduplicated through two LDS hash tables in the candidate buffer: T keeps the
+                //      slot that claimed each entry, T2 the round's winning lane.  A record is kept
+                //      only if its entry was free and it won the round: duplicates and collisions are
+                //      dropped (any subset of distinct particles bounds).  Instead of each lane's
+                //      k-th smallest seed distance (a KMAX-slot fp32 network per seed: 40 % of the
+                //      k = 50 kernel), every lane counts the seeds within 8 radii spread over
+                //      [max_c D(c) - |v - c|, min_c D(c) + |v - c|] and takes the smallest radius
+                //      that holds k of them (2 VALU per seed and radius). ----
+                uint32_t *T = reinterpret_cast<uint32_t *>(buf);
+                uint32_t *T2 = T + 512;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) T[i * 64 + lane] = 0xffffffffu;
+                const int jx0 = __builtin_amdgcn_readfirstlane(cx >> kLatticeShift);
+                const int jy0 = __builtin_amdgcn_readfirstlane(cy >> kLatticeShift);
+                const int jz0 = __builtin_amdgcn_readfirstlane((cz - a.lz0) >> kLatticeShift);
+                // the lane's bracket [lo, hi] of its k-th distance, and Ms >= |seed - tile centre|
+                // for every seed (the corner lists lie within D(c) of their corner)
+                double lo = 0.0, hi = INFINITY, msc = 0.0;
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                    const int jx = min(jx0 + (c & 1), a.cb.n[0] - 1);
+                    const int jy = min(jy0 + ((c >> 1) & 1), a.cb.n[1] - 1);
+                    const int jz = min(jz0 + (c >> 2), a.cb.n[2] - 1);
+                    const double D = a.cb.dk[((size_t)jz * a.cb.n[1] + jy) * a.cb.n[0] + jx];
+                    const double ex = qx - a.cb.ax[jx], ey = qy - a.cb.ay[jy], ez = qz - a.cb.az[jz];
+                    const double e = sqrt((ex * ex + ey * ey) + ez * ez);
+                    lo = fmax(lo, D - e);
+                    hi = fmin(hi, D + e);
+                    const double fx = a.cb.ax[jx] - tcx, fy = a.cb.ay[jy] - tcy, fz = a.cb.az[jz] - tcz;
+                    msc = fmax(msc, D + fabs(fx) + fabs(fy) + fabs(fz));
+                }
+                const double Ms = uniform(msc) * (1.0 + 1e-6) + bhalf;
+                // fp32 seed-voxel distance error: coordinates within Ms of the centre (see the k <= 8 path)
+                const double dl = Ms * 1.9073486328125e-06;
+                const double err = (2.0 * Ms * dl + dl * dl) * (1.0 + 1e-12);
+                const bool bracket = active && hi < INFINITY && lo < hi;
+                double rt[8];   // the radii
+                float tf[8];    // a seed counts at radius i when its fp32 d2 <= tf[i] (it is then within rt[i])
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    rt[i] = bracket ? lo + (hi - lo) * (double)(i + 1) * 0.125 : 0.0;
+                    const double t2 = (rt[i] * rt[i]) * (1.0 - 1e-12) - err;
+                    // (1 - 2^-19) covers the fp32 distance's relative error (2^-20, as below) and the
+                    // rounding of this conversion
+                    tf[i] = bracket && t2 > 0.0 ? (float)(t2 * (1.0 - 1.9073486328125e-06)) : -1.0f;
+                }
+                int cnt[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) cnt[i] = 0;
+                int nb = 0;
+                auto count = [&]() {
+                    wave_lds_sync();
+                    for (int i = 0; i < nb; i += 2) {
+                        const float2 X = *reinterpret_cast<const float2 *>(fbx + i);
+                        const float2 Y = *reinterpret_cast<const float2 *>(fby + i);
+                        const float2 Z = *reinterpret_cast<const float2 *>(fbz + i);
+                        const f32x2 ex = qf2x - f32x2{X.x, X.y}, ey = qf2y - f32x2{Y.x, Y.y}, ez = qf2z - f32x2{Z.x, Z.y};
+                        f32x2 s2 = ex * ex;
+                        s2 = __builtin_elementwise_fma(ey, ey, s2);
+                        s2 = __builtin_elementwise_fma(ez, ez, s2);
+                        const float xs[2] = {s2.x, i + 1 < nb ? s2.y : INFINITY};
+#pragma unroll
+                        for (int u = 0; u < 2; ++u) {
+#pragma unroll
+                            for (int r = 0; r < 8; ++r) cnt[r] += xs[u] <= tf[r] ? 1 : 0;
+                        }
+                    }
+                    nb = 0;
+                    wave_lds_sync();
+                };
+                const int ks = a.seed_n;
+                for (int c = 0; c < 8; ++c) {
+                    const int jx = min(jx0 + (c & 1), a.cb.n[0] - 1);
+                    const int jy = min(jy0 + ((c >> 1) & 1), a.cb.n[1] - 1);
+                    const int jz = min(jz0 + (c >> 2), a.cb.n[2] - 1);
+                    const size_t base = (((size_t)jz * a.cb.n[1] + jy) * a.cb.n[0] + jx) * a.k;
+                    // corner - tile centre (fp32 rounding covered by dl)
+                    const float ocx = (float)(a.cb.ax[jx] - tcx), ocy = (float)(a.cb.ay[jy] - tcy),
+                                ocz = (float)(a.cb.az[jz] - tcz);
+                    for (int e0 = 0; e0 < ks; e0 += 64) {
+                        const int e = e0 + lane;
+                        const float4 rec = e < ks ? a.cb.recs[base + e] : make_float4(0.f, 0.f, 0.f, __uint_as_float(0xffffffffu));
+                        const uint32_t sl = __float_as_uint(rec.w);
+                        const uint32_t h = (sl * 2654435761u) >> 23;  // 512 entries
+                        wave_lds_sync();                               // the previous round's claims
+                        const bool freeh = sl != 0xffffffffu && T[h] == 0xffffffffu;
+                        const uint32_t tag = (uint32_t)(((c * 2 + (e0 >> 6)) << 6) + lane);
+                        if (freeh) T2[h] = tag;
+                        wave_lds_sync();
+                        const bool win = freeh && T2[h] == tag;
+                        if (win) T[h] = sl;
+                        const unsigned long long wm = __builtin_amdgcn_ballot_w64(win);
+                        if (win) {
+                            const int pos = nb + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(wm >> 32),
+                                                                                __builtin_amdgcn_mbcnt_lo((unsigned)wm, 0u));
+                            fbx[pos] = rec.x + ocx;
+                            fby[pos] = rec.y + ocy;
+                            fbz[pos] = rec.z + ocz;
+                        }
+                        nb += __builtin_popcountll(wm);
+                        if (nb > kCap - 64) count();
+                    }
+                }
+                if (nb > 0) count();
+                // the smallest radius holding k distinct seeds
+                double rsel = INFINITY;
+#pragma unroll
+                for (int i = 7; i >= 0; --i)
+                    if (cnt[i] >= a.k) rsel = rt[i];
+                if (active && rsel < INFINITY) {
+                    const double st2 = rsel * rsel * (1.0 + 1e-12);
+                    if (st2 < ub2) {
+                        ub2 = st2;
+                        ub = sqrt_up(st2);
+                    }
+                }
+                if (__builtin_amdgcn_ballot_w64(active && !(rsel < INFINITY)) != 0) {
+                    const double u = lattice_ub();  // no radius held k seeds: the lattice bound
                     if (u < ub) {
                         ub = u;
                         ub2 = u * u;
@@ -1086,6 +1219,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
         if constexpr (KEYS) {
             // an upper bound on the k-th distance (the lattice only ever needs one)
             U[vo] = sqrt(kth2()) * (1.0 + 0x1p-50);
+            if (a.kd_recs != nullptr) {
+                // the first k entries' records seed the next finer level (any k distinct particles
+                // do: list order need not be exact here), in blocks of 8 gathers
+                float4 *o = a.kd_recs + vo * (size_t)a.k;
+#pragma unroll
+                for (int j0 = 0; j0 < KMAX; j0 += 8) {
+                    double4 rec[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const int j = min(j0 + i, KMAX - 1);
+                        const bool ok = bd[j] >= 0.0 && bd[j] < INFINITY;
+                        rec[i] = prec[ok ? key_slot(bd[j], a.smask) : 0u];
+                    }
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const int j = j0 + i;
+                        if (j < KMAX - 1 && j >= a.kpad) {
+                            const bool ok = bd[j] >= 0.0 && bd[j] < INFINITY;
+                            o[j - a.kpad] = make_float4(ok ? (float)(rec[i].x - qx) : 0.f, ok ? (float)(rec[i].y - qy) : 0.f,
+                                                        ok ? (float)(rec[i].z - qz) : 0.f,
+                                                        __uint_as_float(ok ? key_slot(bd[j], a.smask) : 0xffffffffu));
+                        }
+                    }
+                }
+            }
         } else {
             U[vo] = sqrt(bd[KMAX - 1]);
             if (a.kd_recs != nullptr) {

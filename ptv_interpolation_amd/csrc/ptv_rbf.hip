@@ -513,6 +513,240 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M <= 32 ? 3
 }
 
 // ---------------------------------------------------------------------------
+// Systems of 64 < m <= 128 (k_rbf_local keeps a row per lane, so 64 rows at most): one wave
+// per voxel with the m x (m + 3) augmented matrix in (dynamic) LDS and explicit row swaps.
+// The same entries (build_entries' formulas), LAPACK's idamax pivot (largest |a|, lowest row
+// among equal ones), dgetf2's reciprocal multipliers (elim_multiplier), fma updates, the
+// reciprocal back substitution and the segment-sum evaluation of k_rbf_local.  A rare
+// configuration (k >= ~60 with a polynomial, or k >= 65): correctness over speed.
+// ---------------------------------------------------------------------------
+constexpr int kRbfBigRows = 128;
+
+size_t rbf_big_lds_bytes(int m) {
+    return (size_t)m * (m + 3) * sizeof(double) + 3 * kRbfBigRows * sizeof(double4) + kRbfBigRows * sizeof(uint32_t);
+}
+
+__global__ __launch_bounds__(64) void k_rbf_big(RbfKernelArgs a, const double4 *__restrict__ prec,
+                                                const double4 *__restrict__ pval, const uint32_t *__restrict__ slots,
+                                                const double *__restrict__ ax, const double *__restrict__ ay,
+                                                const double *__restrict__ az, const double *__restrict__ qpx,
+                                                const double *__restrict__ qpy, const double *__restrict__ qpz,
+                                                const double *__restrict__ smooth, const int *__restrict__ pw,
+                                                const uint8_t *__restrict__ mask, double *__restrict__ U,
+                                                double *__restrict__ V, double *__restrict__ W,
+                                                int *__restrict__ status) {
+    extern __shared__ double lds_big[];
+    const int lane = threadIdx.x;
+    const int k = a.k, m = a.m, ld = m + 3;
+    double *A = lds_big;                                             // row i at A + i * ld
+    double4 *ye = reinterpret_cast<double4 *>(A + (size_t)m * ld);   // eps-scaled (x, y, z, id), id order
+    double4 *yh = ye + kRbfBigRows;                                  // yhat, id order
+    double4 *sv = yh + kRbfBigRows;                                  // values, later the solution
+    uint32_t *sid = reinterpret_cast<uint32_t *>(sv + kRbfBigRows);  // ids in list order
+
+    const long long plane = (long long)a.nx * a.ny;
+    const long long v = blockIdx.x;  // chunk-local voxel (the grid is exactly the chunk)
+    const int iz = a.z0 + (int)(v / plane);
+    const long long rem = v % plane;
+    const int iy = (int)(rem / a.nx), ix = (int)(rem % a.nx);
+    const size_t vfull = (size_t)iz * plane + rem;
+    const size_t vo = (size_t)(iz - a.out_z0) * plane + rem;
+    if (mask != nullptr && mask[vfull] == 0) {  // wave-uniform (one voxel per wave)
+        if (lane == 0) {
+            U[vo] = 0.0;
+            V[vo] = 0.0;
+            W[vo] = 0.0;
+        }
+        return;
+    }
+    const double eps = a.epsilon;
+
+    // ---- 1. the k neighbours (two per lane), ranked by particle index ----
+    double4 r[2], d[2];
+    uint32_t id[2];
+    double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int j = lane + 64 * h;
+        r[h] = make_double4(0.0, 0.0, 0.0, 0.0);
+        d[h] = r[h];
+        id[h] = 0xffffffffu;
+        if (j < k) {
+            const uint32_t s = slots[(size_t)v * k + j];
+            r[h] = prec[s];
+            d[h] = pval[s];
+            id[h] = (uint32_t)r[h].w;
+            mn[0] = fmin(mn[0], r[h].x);
+            mn[1] = fmin(mn[1], r[h].y);
+            mn[2] = fmin(mn[2], r[h].z);
+            mx[0] = fmax(mx[0], r[h].x);
+            mx[1] = fmax(mx[1], r[h].y);
+            mx[2] = fmax(mx[2], r[h].z);
+        }
+        if (j < kRbfBigRows) sid[j] = id[h];
+    }
+    double sh[3], scl[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const double lo = seg_min<64>(mn[c]), hi = seg_max<64>(mx[c]);
+        sh[c] = (hi + lo) / 2.0;  // _build_system: shift = (max + min)/2, scale = (max - min)/2 (0 -> 1)
+        scl[c] = (hi - lo) / 2.0;
+        if (scl[c] == 0.0) scl[c] = 1.0;
+    }
+    rbf_wave_sync();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int j = lane + 64 * h;
+        if (j < k) {
+            int rank = 0;
+            for (int t = 0; t < k; ++t) {
+                const uint32_t o = sid[t];
+                rank += (o < id[h] || (o == id[h] && t < j)) ? 1 : 0;
+            }
+            ye[rank] = make_double4(r[h].x * eps, r[h].y * eps, r[h].z * eps, (double)id[h]);
+            yh[rank] = make_double4((r[h].x - sh[0]) / scl[0], (r[h].y - sh[1]) / scl[1], (r[h].z - sh[2]) / scl[2], 0.0);
+            sv[rank] = d[h];
+        }
+    }
+    rbf_wave_sync();
+
+    // ---- 2. the augmented system, row by row (lanes over the columns and the 3 right-hand sides) ----
+    for (int i = 0; i < m; ++i) {
+        const bool krow = i < k;
+        const double4 yi = krow ? ye[i] : make_double4(0.0, 0.0, 0.0, 0.0);
+        const double4 hi = krow ? yh[i] : make_double4(0.0, 0.0, 0.0, 0.0);
+        const int tcode = krow ? 0 : pw[i - k];
+        double si = 0.0;
+        if (krow) si = smooth != nullptr ? smooth[(size_t)yi.w] : a.smoothing;
+        for (int j = lane; j < ld; j += 64) {
+            double e = 0.0;
+            if (j < m) {
+                if (krow) {
+                    if (j < k) {
+                        const double4 yj = ye[j];
+                        const double dx = yi.x - yj.x, dy = yi.y - yj.y, dz = yi.z - yj.z;
+                        e = rbf_phi_rt(a.kernel, sqrt((dx * dx + dy * dy) + dz * dz));
+                        if (j == i) e = e + si;
+                    } else {
+                        e = mono(hi.x, hi.y, hi.z, pw[j - k]);
+                    }
+                } else if (j < k) {
+                    const double4 hj = yh[j];
+                    e = mono(hj.x, hj.y, hj.z, tcode);
+                }
+            } else if (krow) {
+                const double4 dv = sv[i];
+                e = j == m ? dv.x : (j == m + 1 ? dv.y : dv.z);
+            }
+            A[(size_t)i * ld + j] = e;
+        }
+    }
+    rbf_wave_sync();
+
+    // ---- 3. LU with partial pivoting (explicit row swaps), the right-hand sides along ----
+    bool singular = false;
+    for (int c = 0; c < m; ++c) {
+        double best = -1.0;
+        int brow = m;
+        for (int i = c + lane; i < m; i += 64) {
+            const double q = fabs(A[(size_t)i * ld + c]);
+            if (q > best) {  // rows ascend per lane: the first maximum is the lowest row
+                best = q;
+                brow = i;
+            }
+        }
+        const double bmax = seg_max<64>(best);
+        const int p = -(int)seg_max<64>(best == bmax ? -(double)brow : -(double)m);  // lowest row holding it
+        singular = singular || !(bmax > 0.0);
+        if (p != c) {
+            for (int j = lane; j < ld; j += 64) {
+                const double t = A[(size_t)c * ld + j];
+                A[(size_t)c * ld + j] = A[(size_t)p * ld + j];
+                A[(size_t)p * ld + j] = t;
+            }
+        }
+        rbf_wave_sync();
+        const double piv = A[(size_t)c * ld + c];
+        for (int i = c + 1 + lane; i < m; i += 64) {
+            const double aic = A[(size_t)i * ld + c];
+            A[(size_t)i * ld + c] = piv != 0.0 ? elim_multiplier(aic, piv) : 0.0;
+        }
+        rbf_wave_sync();
+        for (int j = c + 1 + lane; j < ld; j += 64) {
+            const double pj = A[(size_t)c * ld + j];
+            for (int i = c + 1; i < m; ++i) {
+                const double l = A[(size_t)i * ld + c];
+                A[(size_t)i * ld + j] = fma(-l, pj, A[(size_t)i * ld + j]);
+            }
+        }
+        rbf_wave_sync();
+    }
+
+    // ---- 4. back substitution (column oriented), x_c = b_c * (1 / u_cc) into sv ----
+    for (int c = m - 1; c >= 0; --c) {
+        if (lane == 0) {
+            const double rd = 1.0 / A[(size_t)c * ld + c];
+            sv[c] = make_double4(A[(size_t)c * ld + m] * rd, A[(size_t)c * ld + m + 1] * rd, A[(size_t)c * ld + m + 2] * rd, 0.0);
+        }
+        rbf_wave_sync();
+        const double4 xc = sv[c];
+        for (int i = lane; i < c; i += 64) {
+            const double u = A[(size_t)i * ld + c];
+            A[(size_t)i * ld + m] = fma(-u, xc.x, A[(size_t)i * ld + m]);
+            A[(size_t)i * ld + m + 1] = fma(-u, xc.y, A[(size_t)i * ld + m + 1]);
+            A[(size_t)i * ld + m + 2] = fma(-u, xc.z, A[(size_t)i * ld + m + 2]);
+        }
+        rbf_wave_sync();
+    }
+
+    // ---- 5. evaluate at the voxel ----
+    double qx, qy, qz;
+    if (a.separable) {
+        qx = ax[ix];
+        qy = ay[iy];
+        qz = az[iz];
+    } else {
+        qx = qpx[vfull];
+        qy = qpy[vfull];
+        qz = qpz[vfull];
+    }
+    double o[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int j = lane + 64 * h;
+        double e = 0.0;
+        if (j < k) {
+            const double4 yj = ye[j];
+            const double dx = qx * eps - yj.x, dy = qy * eps - yj.y, dz = qz * eps - yj.z;
+            e = rbf_phi_rt(a.kernel, sqrt((dx * dx + dy * dy) + dz * dz));
+        } else if (j < m) {
+            e = mono((qx - sh[0]) / scl[0], (qy - sh[1]) / scl[1], (qz - sh[2]) / scl[2], pw[j - k]);
+        }
+        if (j < m) {
+            const double4 cf = sv[j];
+            o[0] += e * cf.x;
+            o[1] += e * cf.y;
+            o[2] += e * cf.z;
+        }
+    }
+    double o0 = seg_sum<64>(o[0]), o1 = seg_sum<64>(o[1]), o2 = seg_sum<64>(o[2]);
+    if (lane != 0) return;
+    if (singular) {
+        atomicAdd(&status[0], 1);
+        atomicMin(&status[1], (int)min((long long)vfull, 0x7fffffffLL));
+    }
+    if (a.flags & PTV_FLAG_NAN_TO_NUM) {
+        auto fix = [](double x) { return x != x ? 0.0 : (x == INFINITY ? DBL_MAX : (x == -INFINITY ? -DBL_MAX : x)); };
+        o0 = fix(o0);
+        o1 = fix(o1);
+        o2 = fix(o2);
+    }
+    U[vo] = o0;
+    V[vo] = o1;
+    W[vo] = o2;
+}
+
+// ---------------------------------------------------------------------------
 // Symmetric positive definite systems: kernel gaussian / inverse_multiquadric /
 // inverse_quadratic with degree -1 (no polynomial block, m = k) and smoothing >= 0.  The
 // matrix [phi(eps |y_i - y_j|) + s delta_ij] is SPD for distinct points, so Gaussian
@@ -1071,7 +1305,7 @@ static bool rbf_spd(const RbfKernelArgs &ka, const double *smooth) {
 
 int rbf_system_size(int m) {
     if (m < 1 || m > kRbfMaxSystem) return 0;
-    return (m + 7) & ~7;
+    return m <= 64 ? (m + 7) & ~7 : m;  // k_rbf_local pads to a multiple of 8; k_rbf_big takes m
 }
 
 template <int M>
@@ -1102,6 +1336,15 @@ int launch_rbf(const RbfKernelArgs &ka, const Binned &b, const uint32_t *slots, 
     if ((nvox + 3) / 4 > 0x7fffffffLL) {
         set_error("grid chunk too large for one launch");
         return PTV_E_ARG;
+    }
+    if (M > 64) {
+        const size_t bytes = rbf_big_lds_bytes(ka.m);
+        PTV_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rbf_big),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+        hipLaunchKernelGGL(k_rbf_big, dim3((unsigned)nvox), dim3(64), bytes, s, ka, b.prec, b.pval, slots, ax, ay, az,
+                           qx, qy, qz, smooth, pw, mask, U, V, W, status);
+        PTV_HIP(hipGetLastError());
+        return PTV_OK;
     }
     if (rbf_spd(ka, smooth)) {
         const char *e = dev_knob("PTV_RBF_SPD");  // dev knob: 1 = the LDS-broadcast SPD kernel

@@ -14,7 +14,7 @@ fallback: a missing library or GPU raises.
 
 Supported: ``neighbors`` set (the only way interpolate_field calls it), three
 value components (u, v, w; fewer are zero-padded, more are evaluated in groups
-of three), ``k + #monomials <= 64``.  ``neighbors=None`` (one global system
+of three), ``k + #monomials <= 128``.  ``neighbors=None`` (one global system
 over all particles) is not a GPU path and raises NotImplementedError.
 """
 from __future__ import annotations
@@ -31,7 +31,7 @@ AVAILABLE = {"linear", "thin_plate_spline", "cubic", "quintic", "multiquadric", 
              "inverse_quadratic", "gaussian"}
 SCALE_INVARIANT = {"linear", "thin_plate_spline", "cubic", "quintic"}
 NAME_TO_MIN_DEGREE = {"multiquadric": 0, "linear": 0, "thin_plate_spline": 1, "cubic": 1, "quintic": 2}
-MAX_SYSTEM = 64  # include/ptv_api.h: k + C(degree + 3, 3) <= 64
+MAX_SYSTEM = 128  # include/ptv_api.h: k + C(degree + 3, 3) <= 128
 
 
 def _device():

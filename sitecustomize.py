@@ -21,9 +21,23 @@ _ROOT = os.path.dirname(os.path.abspath(__file__))
 _SHADOWED = ("interpolator", "filtering", "physics")
 
 
+def _reference_shadows(name):
+    """The first other ``name.py`` on sys.path sits next to a ``main.py`` (the reference layout).
+    Any other module of that name is left alone; with none, the normal import finds the shim."""
+    for d in sys.path:
+        d = os.path.abspath(d or os.getcwd())
+        if d == _ROOT:
+            continue
+        if os.path.isfile(os.path.join(d, name + ".py")):
+            return os.path.isfile(os.path.join(d, "main.py"))
+    return False
+
+
 class _DropInFinder(importlib.abc.MetaPathFinder):
     def find_spec(self, name, path=None, target=None):
         if path is not None or name not in _SHADOWED or os.environ.get("PTV_DROPIN", "1") == "0":
+            return None
+        if not _reference_shadows(name):
             return None
         return importlib.util.spec_from_file_location(name, os.path.join(_ROOT, name + ".py"))
 
@@ -43,8 +57,9 @@ def _chain_next_sitecustomize():
             mod = importlib.util.module_from_spec(spec)
             try:
                 spec.loader.exec_module(mod)
-            except Exception:  # a failing system hook must not break start-up
-                pass
+            except Exception as e:  # reported like site.py does, without breaking start-up
+                print(f"Error in sitecustomize {f}; set PYTHONVERBOSE for traceback:\n"
+                      f"{type(e).__name__}: {e}", file=sys.stderr)
             return
 
 

@@ -127,6 +127,31 @@ def test_random_vs_oracle(ctx, kernel, k, degree, eps):
         assert normwise(a, b) <= TOL
 
 
+@pytest.mark.parametrize("kernel,k,degree,eps", [
+    ("thin_plate_spline", 64, None, None),   # m = 68: the reference default kernel past 64
+    ("quintic", 60, None, None),             # m = 70
+    ("cubic", 100, None, None),              # m = 104
+    ("linear", 124, None, None),             # m = 128, the largest system
+    ("inverse_multiquadric", 90, -1, 0.8),   # SPD kernel past the register kernels' 32
+])
+def test_large_systems_vs_oracle(ctx, kernel, k, degree, eps):
+    """Systems of 64 < m <= 128 (k_rbf_big: one wave per voxel, the system in LDS) against the
+    oracle; RBFInterpolator(neighbors=k) accepts any k (interpolator.py:162-167)."""
+    from oracle import cpu_ref
+    from ptv_interpolation_amd.rbf import LocalRBFInterpolator
+
+    P, Q, ax = _rand_case(k * 11 + len(kernel), 5000, 8)
+    it = LocalRBFInterpolator(P, Q, neighbors=k, kernel=kernel, epsilon=eps, degree=degree)
+    U, V, W = it.evaluate_grid(ax, ax, ax)
+    ref = cpu_ref.rbf_local_grid(P, Q, ax, ax, ax, k, kernel, eps, degree)
+    for a, b in zip((U, V, W), ref):
+        err = normwise(a, b)
+        print(f"{kernel} k={k}: normwise {err:.2e}")
+        assert err <= TOL
+    with pytest.raises(NotImplementedError):
+        LocalRBFInterpolator(P, Q, neighbors=126, kernel="quintic")  # m = 136 > 128
+
+
 def test_smoothing_scalar_and_per_point(ctx):
     from oracle import cpu_ref
     from ptv_interpolation_amd.rbf import LocalRBFInterpolator

@@ -15,13 +15,13 @@ run() {  # name, time limit, bench args...
 }
 run headline 300
 run nearest 300 --method nearest --no-e2e
-run sibson 300 --method sibson --k 30 --no-e2e --no-cpu-baseline
-run idw_k50 400 --method idw --k 50 --steps 5 --warmup 1 --no-e2e --no-cpu-baseline
+run sibson 300 --method sibson --k 30 --no-e2e
+run idw_k50 400 --method idw --k 50 --steps 5 --warmup 1 --no-e2e
 run c2 300 --config c2
 run c2r 300 --config c2r
 run c3 600 --config c3
 run c4 600 --config c4 --steps 5 --warmup 1
-run c5 900 --config c5 --steps 3 --warmup 1 --no-cpu-baseline
+run c5 900 --config c5 --steps 3 --warmup 1
 run linear 600 --method linear --steps 10 --warmup 2
 run filter 300 --method filter
 run mask 300 --method mask

@@ -73,7 +73,12 @@ def main(out, rnd):
         gmax = max(k[2] for k, _ in ks)
         return [v for k, v in ks if k[2] == gmax]
 
+    import hashlib
+
+    lib = os.path.join(ROOT, "ptv_interpolation_amd", "libptv_amd.so")
+    sha = hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16] if os.path.exists(lib) else None
     res = {"round": rnd, "kernel": "k_knn_interp<8> (main launch)", "units": "bytes per launch",
+           "lib_sha256": sha,  # the library these counters were collected with (bench.py compares)
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; "
                      "read = 2*FETCH_SIZE*1024 (gfx950 half-count of coalesced streams; the "
                      "k-NN gathers are 32-B double4 loads, uncalibrated), write = WRITE_SIZE*1024"}
