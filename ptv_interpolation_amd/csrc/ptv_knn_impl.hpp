@@ -833,6 +833,63 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                 stamp(t_seed);
             }
         }
+        if constexpr (MODE == kModeFilter) {
+            // ---- seeds (outlier filter, filtering.py:26): the tile's queries are 64 distinct
+            //      particles of one Morton blob, so every lane's k-th (= k + 1 of the filter)
+            //      smallest distance to the tile's real queries bounds its own k-th neighbour
+            //      distance; the padding queries (q_orig ~0, repeats of the last particle) are
+            //      left out. ----
+            const bool realq = active && a.fe.q_orig[vfull] != 0xffffffffu;
+            const unsigned long long rm = __builtin_amdgcn_ballot_w64(realq);
+            const int nu = __builtin_popcountll(rm);
+            if (realq) {
+                const int pos = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(rm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)rm, 0u));
+                fbx[pos] = qfx;
+                fby[pos] = qfy;
+                fbz[pos] = qfz;
+            }
+            // |fp32 coordinate - exact| <= |q - centre| 2^-24 per axis: within Ms * 2^-19 overall
+            const double pmq = realq ? ((double)fabsf(qfx) + (double)fabsf(qfy) + (double)fabsf(qfz)) * (1.0 + 1e-6) : 0.0;
+            const double Ms = 2.0 * uniform(wave_max(pmq)) + bhalf;
+            wave_lds_sync();
+            float sd[KMAX];
+#pragma unroll
+            for (int q = 0; q < KMAX; ++q) sd[q] = INFINITY;
+            for (int i = 0; i < nu; i += 2) {
+                const float2 X = *reinterpret_cast<const float2 *>(fbx + i);
+                const float2 Y = *reinterpret_cast<const float2 *>(fby + i);
+                const float2 Z = *reinterpret_cast<const float2 *>(fbz + i);
+                const f32x2 ex = qf2x - f32x2{X.x, X.y}, ey = qf2y - f32x2{Y.x, Y.y}, ez = qf2z - f32x2{Z.x, Z.y};
+                f32x2 s2 = ex * ex;
+                s2 = __builtin_elementwise_fma(ey, ey, s2);
+                s2 = __builtin_elementwise_fma(ez, ez, s2);
+                const float xs[2] = {s2.x, i + 1 < nu ? s2.y : INFINITY};
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+#pragma unroll
+                    for (int q = KMAX - 1; q > 0; --q) sd[q] = __builtin_amdgcn_fmed3f(sd[q - 1], sd[q], xs[u]);
+                    sd[0] = fminf(sd[0], xs[u]);
+                }
+            }
+            float kth = sd[0];
+#pragma unroll
+            for (int q = 1; q < KMAX; ++q)
+                if (q == a.k - 1) kth = sd[q];
+            if (active && kth < INFINITY) {
+                const double dl = Ms * 1.9073486328125e-06;
+                const double st2 = ((double)kth * (1.0 + 9.5367431640625e-07) + (2.0 * Ms * dl + dl * dl)) * (1.0 + 1e-12);
+                if (st2 < ub2) {
+                    ub2 = st2;
+                    ub = sqrt_up(st2);
+                }
+            }
+            // the per-lane bounds prune candidates; the gather radius still starts at the density
+            // radius (a Morton blob can be split, and its worst lane would set a huge radius)
+            seeded = false;
+            thr = dmin(kth2(), ub2);
+            wave_lds_sync();  // the gather reuses the candidate buffers
+            stamp(t_seed);
+        }
         double cpass = 0.0;
         float thrf = 0.f;
         double Rp = -1.0;  // radius already gathered (none yet)

@@ -7,8 +7,9 @@ tag=${1:-r02}
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 out=gpurun_out/${tag}_lines
 mkdir -p "$out"
-run() {  # name, time limit, bench args...
+run() {  # name, time limit, bench args...  (LINES="a b c" runs only those)
   local name=$1 lim=$2; shift 2
+  if [ -n "$LINES" ] && [[ " $LINES " != *" $name "* ]]; then return 0; fi
   echo "== $name: bench.py $*"
   timeout -k 10 "$lim" python -u bench.py "$@" > "$out/$name.json" 2> "$out/$name.err" || { echo "FAILED $name"; tail -5 "$out/$name.err"; exit 1; }
   tail -c 400 "$out/$name.json"; echo
