@@ -275,7 +275,15 @@ namespace {
 // gave k-NN 14.9 ms against 16.3 ms for cubic cells of 5.5, the lattice 2.31 against 2.44
 constexpr double kDefaultOccupancySmallK = 16.0;  // particles per (y, z) cell column segment
 constexpr double kDefaultXRefSmallK = 12.0;       // x-refinement of the k <= 8 cells
-constexpr double kDefaultOccupancy = 1.2;
+constexpr double kDefaultOccupancy = 1.2;          // k > 8 without lattice seeds (point lists)
+// k > 8 with union seeds (round 3, tools/gpu_knob_sweep.sh, 512^3 / 5M IDW k = 50): the seeded
+// gather radius is tight, so coarser cells (fewer runs per row) win again: main launch
+// 139.7 ms at 1.2 / cubic, 137.7 at 2.5, 134.8 at 5, 133.5 at 8 with x 4x thinner, 133.4 at 16 / 12
+constexpr double kDefaultOccupancyLargeK = 8.0;
+constexpr double kDefaultXRefLargeK = 4.0;
+// the outlier filter's particle queries (5M, k = 25): 23.3 ms at 1.2, 22.6 at 2.5, 22.4 at 5,
+// 24.1 at 8 / 4, 28.4 at 16 / 12
+constexpr double kFilterOccupancy = 5.0;
 constexpr double kDefaultR0Scale = 1.0;     // first gather radius / expected k-NN radius
 constexpr long long kMaxCells = 1LL << 28;
 constexpr long long kLatticeStopPoints = 50000; // no coarser lattice below this many points
@@ -460,9 +468,12 @@ int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchP
 
     // 2. binning
     const bool small_k = kmax_for(prm->k) <= 8;
-    const double occ = prm->cell_occupancy > 0.0 ? prm->cell_occupancy
-                       : (small_k ? kDefaultOccupancySmallK : kDefaultOccupancy);
-    CellGrid cg = make_cell_grid(lo, hi, n, occ, small_k && !(prm->cell_occupancy > 0.0) ? kDefaultXRefSmallK : 1.0);
+    const bool seeded_lattice = sep && prm->lattice_bounds >= 0;  // union seeds bound the large-k search
+    const bool given = prm->cell_occupancy > 0.0;
+    const double occ = given ? prm->cell_occupancy
+                       : (small_k ? kDefaultOccupancySmallK : (seeded_lattice ? kDefaultOccupancyLargeK : kDefaultOccupancy));
+    const double xref = given ? 1.0 : (small_k ? kDefaultXRefSmallK : (seeded_lattice ? kDefaultXRefLargeK : 1.0));
+    CellGrid cg = make_cell_grid(lo, hi, n, occ, xref);
     const size_t m = (size_t)cg.ncells;
     PTV_TRY(c->code.ensure(2 * (size_t)n));  // cell codes + in-cell ranks (launch_bin)
     PTV_TRY(c->perm.ensure(n));
@@ -1588,7 +1599,7 @@ int run_filter(ptv_ctx *c, const ptv_particles *p, const ptv_filter_params *prm,
     g.pz = c->qpts[2].p;
     g.z_begin = 0;
     g.z_end = g.nz;
-    double r0s = 0.0, occ = 0.0;
+    double r0s = 0.0, occ = kFilterOccupancy;
     if (const char *e = dev_knob("PTV_FILTER_R0")) r0s = std::atof(e);       // dev knobs
     if (const char *e = dev_knob("PTV_FILTER_OCC")) occ = std::atof(e);
     const SearchParams sp{PTV_METHOD_IDW, prm->k + 1, 2.0, 1e-10, 0u, occ, r0s, -1};
