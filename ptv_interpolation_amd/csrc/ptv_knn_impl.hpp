@@ -279,6 +279,13 @@ __device__ __forceinline__ double div_by(double a, double b, double r) {
     return fma(fma(-q, b, a), r, q);
 }
 
+// whether div_by(a, b, RN(1/b)) is the IEEE quotient for every a in {0} u [amin, amax] (amin the
+// smallest nonzero numerator): b in [2^-1000, 2^1000] (1/b finite and normal), the nonzero
+// numerators normal with margin (the residual a - b q exact) and every quotient normal
+__device__ __forceinline__ bool div_by_ok(double amin, double amax, double b) {
+    return b >= 0x1p-1000 && b <= 0x1p1000 && amin >= 0x1p-960 && amin >= b * 0x1p-1000 && amax <= b * 0x1p1000;
+}
+
 // IEEE sqrt for x >= 2^-767: the LLVM gfx9 f64 expansion (rsq seed, two Goldschmidt
 // corrections) without its small-input rescale; tiny, zero and infinite x take sqrt()
 __device__ __forceinline__ double sqrt_cr(double x) {
@@ -1479,6 +1486,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
         if (a.method == PTV_METHOD_SIBSON) {
             // pass 1: d, 1/(d + eps) -> sum (pairwise), sum d -> mean; the order check
             PairwiseStream ps_inv, ps_d;
+            double ivmin = INFINITY, dmax = 0.0, dmin_nz = INFINITY;  // operand ranges for div_by below
 #pragma unroll
             for (int m = 0; m < KMAX; m += 8) {
                 if (m < k) {
@@ -1486,12 +1494,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                     d2_block(m, d2);
 #pragma unroll
                     for (int i = 0; i < 8; ++i) {
+                        dv[i] = sqrt_cr(d2[i]);
+                        iv[i] = 1.0 / (dv[i] + a.eps);
                         if (m + i < k) {
                             ok = ok && !(d2[i] < prev);
                             prev = d2[i];
+                            ivmin = fmin(ivmin, iv[i]);
+                            dmax = fmax(dmax, dv[i]);
+                            if (dv[i] > 0.0) dmin_nz = fmin(dmin_nz, dv[i]);
                         }
-                        dv[i] = sqrt_cr(d2[i]);
-                        iv[i] = 1.0 / (dv[i] + a.eps);
                         if constexpr (KEEP) {
                             if (m + i < KMAX) dk[min(m + i, KMAX - 1)] = dv[i];
                         }
@@ -1533,23 +1544,44 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                 }
             }
             const double den = sqrt(ps_var.finish(k) / (double)k) + a.eps;
+            // the quotients iv / s_inv and -d / den through one reciprocal each (div_by: correctly
+            // rounded for normal operands and quotients; d = 0 gives 0 exactly) when every lane's
+            // operands are in range, IEEE division otherwise
+            const bool fdiv = __builtin_amdgcn_ballot_w64(!(div_by_ok(ivmin, s_inv, s_inv) && div_by_ok(dmin_nz, dmax, den))) == 0;
+            const double rsi = 1.0 / s_inv, rden = 1.0 / den;
             auto w_block = [&](int m, double (&w)[8]) {
                 double dv[8];
                 d_block(m, dv);
 #pragma unroll
-                for (int i = 0; i < 8; ++i) w[i] = (1.0 / (dv[i] + a.eps)) / s_inv * exp(-dv[i] / den);
+                for (int i = 0; i < 8; ++i) {
+                    const double iv = 1.0 / (dv[i] + a.eps);
+                    w[i] = fdiv ? div_by(iv, s_inv, rsi) * exp(div_by(-dv[i], den, rden))
+                                : iv / s_inv * exp(-dv[i] / den);
+                }
             };
-            // pass 3: the exponential weights' sum
+            // pass 3: the exponential weights (kept in place of the distances when the list is
+            // register-held: pass 4 reads them back) and their sum
             PairwiseStream ps_w;
+            double wmin = INFINITY;
 #pragma unroll
             for (int m = 0; m < KMAX; m += 8) {
                 if (m < k) {
                     double w[8];
                     w_block(m, w);
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        if (m + i < k && w[i] > 0.0) wmin = fmin(wmin, w[i]);  // exp underflow: 0 / s2 exact
+                        if constexpr (KEEP) {
+                            if (m + i < KMAX) dk[min(m + i, KMAX - 1)] = w[i];
+                        }
+                    }
                     ps_w.add(m, k, w);
                 }
             }
             const double s2 = ps_w.finish(k);
+            // w / s2 through one reciprocal when s2, the nonzero w and every quotient are normal
+            const bool fast = __builtin_amdgcn_ballot_w64(!div_by_ok(wmin, s2, s2)) == 0;
+            const double rs2 = 1.0 / s2;
             // pass 4: normalised weights times the values
             PairwiseStream pu, pv, pw;
 #pragma unroll
@@ -1558,10 +1590,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                     double4 vv[8];
                     val_block(m, vv);
                     double w[8], tu[8], tv[8], tw8[8];
-                    w_block(m, w);
+                    if constexpr (KEEP) {
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) w[i] = dk[min(m + i, KMAX - 1)];
+                    } else {
+                        w_block(m, w);
+                    }
 #pragma unroll
                     for (int i = 0; i < 8; ++i) {
-                        const double wn = w[i] / s2;
+                        const double wn = fast ? div_by(w[i], s2, rs2) : w[i] / s2;
                         tu[i] = wn * vv[i].x;
                         tv[i] = wn * vv[i].y;
                         tw8[i] = wn * vv[i].z;
@@ -1604,7 +1641,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
             }
             const double s = ps.finish(k);
             // w_j / s through one reciprocal when every quotient is normal (see the k <= 12 path)
-            const bool fast = __builtin_amdgcn_ballot_w64(!(s <= 0x1p1000 && wmin >= s * 0x1p-1000)) == 0;
+            const bool fast = __builtin_amdgcn_ballot_w64(!div_by_ok(wmin, s, s)) == 0;
             const double rs = 1.0 / s;
             // pass 2: normalised weights times the values
             PairwiseStream pu, pv, pw;
@@ -1701,6 +1738,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
         if (a.method == PTV_METHOD_SIBSON) {
             // pass 1: d, 1/(d + eps) -> sum (pairwise), sum d -> mean; the order check
             PairwiseStream ps_inv, ps_d;
+            double ivmin = INFINITY, dmax = 0.0, dmin_nz = INFINITY;  // operand ranges for div_by below
             rewind();
 #pragma unroll 1
             for (int m = 0; m < k; m += 8) {
@@ -1710,12 +1748,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                 d2_block(s8, d2);
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
+                    dv[i] = sqrt_cr(d2[i]);
+                    iv[i] = 1.0 / (dv[i] + a.eps);
                     if (m + i < k) {
                         ok = ok && !(d2[i] < prev);
                         prev = d2[i];
+                        ivmin = fmin(ivmin, iv[i]);
+                        dmax = fmax(dmax, dv[i]);
+                        if (dv[i] > 0.0) dmin_nz = fmin(dmin_nz, dv[i]);
                     }
-                    dv[i] = sqrt_cr(d2[i]);
-                    iv[i] = 1.0 / (dv[i] + a.eps);
                 }
                 ps_inv.add(m, k, iv);
                 ps_d.add(m, k, dv);
@@ -1744,12 +1785,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                 ps_var.add(m, k, t);
             }
             const double den = sqrt(ps_var.finish(k) / (double)k) + a.eps;
+            // iv / s_inv and -d / den through one reciprocal each where div_by_ok (the k <= 32 path)
+            const bool fdiv = __builtin_amdgcn_ballot_w64(!(div_by_ok(ivmin, s_inv, s_inv) && div_by_ok(dmin_nz, dmax, den))) == 0;
+            const double rsi = 1.0 / s_inv, rden = 1.0 / den;
             auto w_of = [&](double d2) {
                 const double d = sqrt_cr(d2);
-                return (1.0 / (d + a.eps)) / s_inv * exp(-d / den);
+                const double iv = 1.0 / (d + a.eps);
+                return fdiv ? div_by(iv, s_inv, rsi) * exp(div_by(-d, den, rden)) : iv / s_inv * exp(-d / den);
             };
             // pass 3: the exponential weights' sum
             PairwiseStream ps_w;
+            double wmin = INFINITY;
             rewind();
 #pragma unroll 1
             for (int m = 0; m < k; m += 8) {
@@ -1758,10 +1804,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                 double d2[8], w[8];
                 d2_block(s8, d2);
 #pragma unroll
-                for (int i = 0; i < 8; ++i) w[i] = w_of(d2[i]);
+                for (int i = 0; i < 8; ++i) {
+                    w[i] = w_of(d2[i]);
+                    if (m + i < k && w[i] > 0.0) wmin = fmin(wmin, w[i]);
+                }
                 ps_w.add(m, k, w);
             }
             const double s2 = ps_w.finish(k);
+            const bool fast = __builtin_amdgcn_ballot_w64(!div_by_ok(wmin, s2, s2)) == 0;
+            const double rs2 = 1.0 / s2;
             // pass 4: normalised weights times the values
             PairwiseStream pu, pv, pw;
             rewind();
@@ -1772,7 +1823,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                 double d2[8], wn[8];
                 d2_block(s8, d2);
 #pragma unroll
-                for (int i = 0; i < 8; ++i) wn[i] = w_of(d2[i]) / s2;
+                for (int i = 0; i < 8; ++i) wn[i] = fast ? div_by(w_of(d2[i]), s2, rs2) : w_of(d2[i]) / s2;
                 double tu[8], tv[8], tw8[8];
                 xyz_block(pval, s8, tu, tv, tw8);
 #pragma unroll
@@ -1818,7 +1869,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
             }
             const double s = ps.finish(k);
             // w_j / s through one reciprocal when every quotient is normal (see the k <= 12 path)
-            const bool fast = __builtin_amdgcn_ballot_w64(!(s <= 0x1p1000 && wmin >= s * 0x1p-1000)) == 0;
+            const bool fast = __builtin_amdgcn_ballot_w64(!div_by_ok(wmin, s, s)) == 0;
             const double rs = 1.0 / s;
             // pass 2: normalised weights times the values
             PairwiseStream pu, pv, pw;
@@ -1927,12 +1978,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
         }
         const double s = pairwise<KMAX>(w, k);
         // w_j / s through one reciprocal when s and every quotient are normal (w_j > 0 here:
-        // s <= 2^1000 and min_j w_j >= s 2^-1000); IEEE division on any lane otherwise
+        // div_by_ok); IEEE division on any lane otherwise
         double wmin = w[0];
 #pragma unroll
         for (int j = 1; j < KMAX; ++j)
             if (j < k) wmin = fmin(wmin, w[j]);
-        const bool fast = s <= 0x1p1000 && wmin >= s * 0x1p-1000;
+        const bool fast = div_by_ok(wmin, s, s);
         if (__builtin_amdgcn_ballot_w64(!fast) == 0) {
             const double rs = 1.0 / s;
 #pragma unroll
