@@ -38,6 +38,7 @@
 #include <cstdlib>
 #include <algorithm>
 #include <cmath>
+#include <utility>
 
 #include "../../include/ptv_api.h"
 #include "ptv_kernels.hpp"
@@ -154,6 +155,145 @@ __device__ __forceinline__ void insert_key(double (&bd)[KMAX], double key) {
         cd = nc;
     }
     asm("v_min_f64 %[bd], %[bd], %[cd]" : [bd] "+v"(bd[KMAX - 1]) : [cd] "v"(cd));
+}
+
+// Batched insertion into a key list: 8 keys sorted by a network, then Batcher's odd-even merge
+// of the sorted list (registers 0 .. KMAX-1) with them (KMAX .. KMAX+7), keeping the KMAX
+// smallest.  The merge leaves the kept outputs in registers 0 .. KMAX-1 in order, and every
+// comparator that only feeds the dropped 8 outputs is removed (one op for those that keep
+// only their min or max): 310 ops for 8 keys at KMAX = 56 against 896 for 8 insert_key sweeps.
+// Keys are distinct (the slot is part of the key), so the list equals the sequential one.
+struct KeyNet {
+    int n;
+    short a[1024], b[1024];
+    unsigned char kind[1024];  // 1: a = min only, 2: b = max only, 3: both
+};
+struct RegList {
+    int n;
+    short r[160];
+};
+constexpr RegList reg_sub(const RegList &x, int start) {
+    RegList o{};
+    o.n = 0;
+    for (int i = start; i < x.n; i += 2) o.r[o.n++] = x.r[i];
+    return o;
+}
+// merge sorted register lists A and B in place (comparators appended to net); out = the sorted
+// register order
+constexpr void net_merge(const RegList &A, const RegList &B, KeyNet &net, RegList &out) {
+    out.n = 0;
+    if (A.n == 0 || B.n == 0) {
+        const RegList &s = A.n == 0 ? B : A;
+        for (int i = 0; i < s.n; ++i) out.r[out.n++] = s.r[i];
+        return;
+    }
+    if (A.n == 1 && B.n == 1) {
+        net.a[net.n] = A.r[0];
+        net.b[net.n] = B.r[0];
+        net.kind[net.n++] = 3;
+        out.r[out.n++] = A.r[0];
+        out.r[out.n++] = B.r[0];
+        return;
+    }
+    RegList v{}, w{};
+    net_merge(reg_sub(A, 0), reg_sub(B, 0), net, v);
+    net_merge(reg_sub(A, 1), reg_sub(B, 1), net, w);
+    out.r[out.n++] = v.r[0];
+    for (int i = 0;; ++i) {
+        const bool hw = i < w.n, hv = i + 1 < v.n;
+        if (hw && hv) {
+            net.a[net.n] = w.r[i];
+            net.b[net.n] = v.r[i + 1];
+            net.kind[net.n++] = 3;
+            out.r[out.n++] = w.r[i];
+            out.r[out.n++] = v.r[i + 1];
+        } else if (hw) {
+            out.r[out.n++] = w.r[i];
+        } else if (hv) {
+            out.r[out.n++] = v.r[i + 1];
+        } else {
+            break;
+        }
+    }
+}
+constexpr void net_sort(const RegList &x, KeyNet &net, RegList &out) {
+    if (x.n <= 1) {
+        out = x;
+        return;
+    }
+    RegList lo{}, hi{}, slo{}, shi{};
+    const int h = x.n / 2;
+    for (int i = 0; i < x.n; ++i) (i < h ? lo.r[lo.n++] : hi.r[hi.n++]) = x.r[i];
+    net_sort(lo, net, slo);
+    net_sort(hi, net, shi);
+    net_merge(slo, shi, net, out);
+}
+template <int KMAX>
+constexpr KeyNet make_key_net() {
+    KeyNet net{};
+    RegList L{}, Bk{}, sb{}, out{};
+    for (int i = 0; i < KMAX; ++i) L.r[L.n++] = (short)i;
+    for (int i = 0; i < 8; ++i) Bk.r[Bk.n++] = (short)(KMAX + i);
+    net_sort(Bk, net, sb);
+    const int nsort = net.n;
+    net_merge(L, sb, net, out);
+    // the kept outputs sit in registers 0 .. KMAX-1 in order (checked here); remove dead ops
+    bool live[KMAX + 8] = {};
+    for (int i = 0; i < KMAX; ++i) {
+        if (out.r[i] != i) net.n = -1;  // not in place: refuse (the static_assert below fires)
+        live[i] = true;
+    }
+    if (net.n < 0) return net;
+    KeyNet res{};
+    int keep[1024] = {};
+    for (int c = net.n - 1; c >= 0; --c) {
+        const bool la = live[net.a[c]], lb = live[net.b[c]];
+        keep[c] = c < nsort ? 3 : (la ? 1 : 0) | (lb ? 2 : 0);
+        if (keep[c]) live[net.a[c]] = live[net.b[c]] = true;
+    }
+    for (int c = 0; c < net.n; ++c)
+        if (keep[c]) {
+            res.a[res.n] = net.a[c];
+            res.b[res.n] = net.b[c];
+            res.kind[res.n++] = (unsigned char)keep[c];
+        }
+    return res;
+}
+template <int KMAX>
+struct KeyNetOf {
+    static constexpr KeyNet net = make_key_net<KMAX>();
+    static_assert(net.n > 0, "merge network outputs not in place");
+};
+template <int KMAX, int C>
+__device__ __forceinline__ void key_net_op(double (&v)[KMAX + 8]) {
+    constexpr int a = KeyNetOf<KMAX>::net.a[C], b = KeyNetOf<KMAX>::net.b[C], kd = KeyNetOf<KMAX>::net.kind[C];
+    const double x = v[a], y = v[b];
+    if constexpr (kd & 1) {
+        double r;
+        asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+        v[a] = r;
+    }
+    if constexpr (kd & 2) {
+        double r;
+        asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+        v[b] = r;
+    }
+}
+template <int KMAX, int... C>
+__device__ __forceinline__ void key_net_run(double (&v)[KMAX + 8], std::integer_sequence<int, C...>) {
+    (key_net_op<KMAX, C>(v), ...);
+}
+// the 8 keys nk (any order, +inf = none) into the sorted list bd
+template <int KMAX>
+__device__ __forceinline__ void insert_keys8(double (&bd)[KMAX], const double (&nk)[8]) {
+    double v[KMAX + 8];
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) v[j] = bd[j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[KMAX + j] = nk[j];
+    key_net_run<KMAX>(v, std::make_integer_sequence<int, KeyNetOf<KMAX>::net.n>{});
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) bd[j] = v[j];
 }
 
 // numpy's pairwise sum (see pairwise()) fed in index order in blocks of 8 values: block m
@@ -979,7 +1119,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                 m &= ~((1ull << (nb - ng)) - 1ull);  // stale slots past nbuf
                 const double4 *gbuf = buf + g0 + nb - 64;  // bit position p <-> gbuf[63 - p]
                 const int nit = __builtin_amdgcn_readfirstlane(wave_max_i(__builtin_popcountll(m)));
-                for (int it = 0; it < nit; ++it) {
+                if constexpr (KEYS && MODE != kModeRadius) {
+                    // key lists: 8 candidates per lane at a time into one merge network
+                    // (insert_keys8); iterations past nit find m = 0 everywhere (+inf keys).
+                    // No exact threshold test: a key past the list's end drops out, and every
+                    // candidate sharing the k-th key's truncation reaches the (k+1)-th slot
+                    // (the near-tie check)
+                    for (int it = 0; it < nit; it += 8) {
+                        n_acc += (uint32_t)min(8, nit - it);
+                        double nk[8];
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            const bool has = m != 0ull;
+                            const int lz = __builtin_clzll(m | 1ull);
+                            m &= ~(0x8000000000000000ull >> lz);
+                            const double4 c = gbuf[lz];
+                            const double dx = qx - c.x, dy = qy - c.y, dz = qz - c.z;
+                            const double e2 = (dx * dx + dy * dy) + dz * dz;
+                            nk[j] = make_key(has, e2, (uint32_t)__double_as_longlong(c.w), a.smask);
+                        }
+                        insert_keys8<KMAX>(bd, nk);
+                    }
+                } else for (int it = 0; it < nit; ++it) {
                     // branch-free body (lanes without bits read a valid stale slot and insert inf)
                     ++n_acc;
                     const bool has = m != 0ull;
@@ -998,12 +1159,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                             rsv += w * val.y;
                             rsw += w * val.z;
                         }
-                    } else if constexpr (KEYS) {
-                        // no exact threshold test: a key at or past the list's end is a no-op, and
-                        // every candidate that shares the k-th key's truncation must reach the
-                        // (k+1)-th slot (the near-tie check)
-                        insert_key<KMAX>(bd, make_key(has, e2, (uint32_t)__double_as_longlong(c.w), a.smask));
-                    } else {
+                    } else if constexpr (!KEYS) {
                         const double d2 = (has && e2 < thr) ? e2 : INFINITY;
                         insert<KMAX>(bd, bp, d2, (int)__double_as_longlong(c.w));  // no-op where d2 = inf
                         thr = dmin(bd[KMAX - 1], ub2);
