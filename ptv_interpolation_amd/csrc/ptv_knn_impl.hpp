@@ -67,6 +67,9 @@ namespace ptv {
 #define PTV_KNN_KEYI_2W 40  // key-list interpolation kernels of at least this many slots: 2 waves per SIMD
 #endif
 
+#ifndef PTV_STAMP_SEEDSPLIT
+#define PTV_STAMP_SEEDSPLIT 0  // dev stamp builds: union-seed counting passes stamped as 'setup'
+#endif
 #ifndef PTV_STAMP_ALL
 #define PTV_STAMP_ALL 0  // dev builds: 1 = the STAMP instantiation for every KMAX (not only 8)
 #endif
@@ -228,17 +231,17 @@ constexpr void net_sort(const RegList &x, KeyNet &net, RegList &out) {
     net_sort(hi, net, shi);
     net_merge(slo, shi, net, out);
 }
-template <int KMAX>
+template <int KMAX, int NB>
 constexpr KeyNet make_key_net() {
     KeyNet net{};
     RegList L{}, Bk{}, sb{}, out{};
     for (int i = 0; i < KMAX; ++i) L.r[L.n++] = (short)i;
-    for (int i = 0; i < 8; ++i) Bk.r[Bk.n++] = (short)(KMAX + i);
+    for (int i = 0; i < NB; ++i) Bk.r[Bk.n++] = (short)(KMAX + i);
     net_sort(Bk, net, sb);
     const int nsort = net.n;
     net_merge(L, sb, net, out);
     // the kept outputs sit in registers 0 .. KMAX-1 in order (checked here); remove dead ops
-    bool live[KMAX + 8] = {};
+    bool live[KMAX + NB] = {};
     for (int i = 0; i < KMAX; ++i) {
         if (out.r[i] != i) net.n = -1;  // not in place: refuse (the static_assert below fires)
         live[i] = true;
@@ -259,14 +262,14 @@ constexpr KeyNet make_key_net() {
         }
     return res;
 }
-template <int KMAX>
+template <int KMAX, int NB>
 struct KeyNetOf {
-    static constexpr KeyNet net = make_key_net<KMAX>();
+    static constexpr KeyNet net = make_key_net<KMAX, NB>();
     static_assert(net.n > 0, "merge network outputs not in place");
 };
-template <int KMAX, int C>
-__device__ __forceinline__ void key_net_op(double (&v)[KMAX + 8]) {
-    constexpr int a = KeyNetOf<KMAX>::net.a[C], b = KeyNetOf<KMAX>::net.b[C], kd = KeyNetOf<KMAX>::net.kind[C];
+template <int KMAX, int NB, int C>
+__device__ __forceinline__ void key_net_op(double (&v)[KMAX + NB]) {
+    constexpr int a = KeyNetOf<KMAX, NB>::net.a[C], b = KeyNetOf<KMAX, NB>::net.b[C], kd = KeyNetOf<KMAX, NB>::net.kind[C];
     const double x = v[a], y = v[b];
     if constexpr (kd & 1) {
         double r;
@@ -279,19 +282,24 @@ __device__ __forceinline__ void key_net_op(double (&v)[KMAX + 8]) {
         v[b] = r;
     }
 }
-template <int KMAX, int... C>
-__device__ __forceinline__ void key_net_run(double (&v)[KMAX + 8], std::integer_sequence<int, C...>) {
-    (key_net_op<KMAX, C>(v), ...);
+template <int KMAX, int NB, int... C>
+__device__ __forceinline__ void key_net_run(double (&v)[KMAX + NB], std::integer_sequence<int, C...>) {
+    (key_net_op<KMAX, NB, C>(v), ...);
 }
-// the 8 keys nk (any order, +inf = none) into the sorted list bd
+#ifndef PTV_KEY_BATCH
+#define PTV_KEY_BATCH 8  // dev builds: keys per merge network
+#endif
 template <int KMAX>
-__device__ __forceinline__ void insert_keys8(double (&bd)[KMAX], const double (&nk)[8]) {
-    double v[KMAX + 8];
+constexpr int key_batch() { return PTV_KEY_BATCH; }
+// the NB keys nk (any order, +inf = none) into the sorted list bd
+template <int KMAX, int NB>
+__device__ __forceinline__ void insert_keys(double (&bd)[KMAX], const double (&nk)[NB]) {
+    double v[KMAX + NB];
 #pragma unroll
     for (int j = 0; j < KMAX; ++j) v[j] = bd[j];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[KMAX + j] = nk[j];
-    key_net_run<KMAX>(v, std::make_integer_sequence<int, KeyNetOf<KMAX>::net.n>{});
+    for (int j = 0; j < NB; ++j) v[KMAX + j] = nk[j];
+    key_net_run<KMAX, NB>(v, std::make_integer_sequence<int, KeyNetOf<KMAX, NB>::net.n>{});
 #pragma unroll
     for (int j = 0; j < KMAX; ++j) bd[j] = v[j];
 }
@@ -869,6 +877,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                 // the lane's bracket [lo, hi] of its k-th distance, and Ms >= |seed - tile centre|
                 // for every seed (the corner lists lie within D(c) of their corner)
                 double lo = 0.0, hi = INFINITY, msc = 0.0;
+                // corner - tile centre in fp32 per axis (the corners take 2 values on each axis;
+                // rounding covered by dl)
+                float ox0 = 0.f, ox1 = 0.f, oy0 = 0.f, oy1 = 0.f, oz0 = 0.f, oz1 = 0.f;  // named: an
+                // array indexed by a select comes back as a scratch array
 #pragma unroll
                 for (int c = 0; c < 8; ++c) {
                     const int jx = min(jx0 + (c & 1), a.cb.n[0] - 1);
@@ -881,6 +893,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                     hi = fmin(hi, D + e);
                     const double fx = a.cb.ax[jx] - tcx, fy = a.cb.ay[jy] - tcy, fz = a.cb.az[jz] - tcz;
                     msc = fmax(msc, D + fabs(fx) + fabs(fy) + fabs(fz));
+                    if (c == 0) {
+                        ox0 = (float)fx;
+                        oy0 = (float)fy;
+                        oz0 = (float)fz;
+                    }
+                    if (c == 1) ox1 = (float)fx;
+                    if (c == 2) oy1 = (float)fy;
+                    if (c == 4) oz1 = (float)fz;
                 }
                 const double Ms = uniform(msc) * (1.0 + 1e-6) + bhalf;
                 // fp32 seed-voxel distance error: coordinates within Ms of the centre (see the k <= 8 path)
@@ -901,7 +921,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
 #pragma unroll
                 for (int i = 0; i < 8; ++i) cnt[i] = 0;
                 int nb = 0;
-                auto count = [&]() {
+                auto count = [&]() __attribute__((always_inline)) {
+#if PTV_STAMP_SEEDSPLIT
+                    stamp(t_seed);  // dev stamp builds: the counting passes go to 'setup'
+#endif
                     wave_lds_sync();
                     for (int i = 0; i < nb; i += 2) {
                         const float2 X = *reinterpret_cast<const float2 *>(fbx + i);
@@ -920,24 +943,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                     }
                     nb = 0;
                     wave_lds_sync();
+#if PTV_STAMP_SEEDSPLIT
+                    stamp(t_setup);
+#endif
                 };
                 const int ks = a.seed_n;
-                for (int c = 0; c < 8; ++c) {
+                // rounds t = 0 .. 8 * rpc - 1 of up to 64 records (corner t / rpc, entries from
+                // (t % rpc) * 64); each round's records are loaded one round ahead
+                const int rpc = (ks + 63) >> 6;
+                const int nrounds = 8 * rpc;
+                const float4 none = make_float4(0.f, 0.f, 0.f, __uint_as_float(0xffffffffu));
+                auto load_round = [&](int t) -> float4 {
+                    const int c = t / rpc, e = (t - c * rpc) * 64 + lane;
                     const int jx = min(jx0 + (c & 1), a.cb.n[0] - 1);
                     const int jy = min(jy0 + ((c >> 1) & 1), a.cb.n[1] - 1);
                     const int jz = min(jz0 + (c >> 2), a.cb.n[2] - 1);
                     const size_t base = (((size_t)jz * a.cb.n[1] + jy) * a.cb.n[0] + jx) * a.k;
-                    // corner - tile centre (fp32 rounding covered by dl)
-                    const float ocx = (float)(a.cb.ax[jx] - tcx), ocy = (float)(a.cb.ay[jy] - tcy),
-                                ocz = (float)(a.cb.az[jz] - tcz);
-                    for (int e0 = 0; e0 < ks; e0 += 64) {
-                        const int e = e0 + lane;
-                        const float4 rec = e < ks ? a.cb.recs[base + e] : make_float4(0.f, 0.f, 0.f, __uint_as_float(0xffffffffu));
+                    return e < ks ? a.cb.recs[base + e] : none;
+                };
+                float4 recn = load_round(0);  // nrounds >= 8
+                for (int t = 0; t < nrounds; ++t) {
+                    const float4 rec = recn;
+                    recn = load_round(min(t + 1, nrounds - 1));  // the last round reloads its own
+                    const int c = t / rpc;
+                    const float ocx = (c & 1) ? ox1 : ox0, ocy = (c & 2) ? oy1 : oy0, ocz = (c & 4) ? oz1 : oz0;
+                    {
                         const uint32_t sl = __float_as_uint(rec.w);
                         const uint32_t h = (sl * 2654435761u) >> 23;  // 512 entries
                         wave_lds_sync();                               // the previous round's claims
                         const bool freeh = sl != 0xffffffffu && T[h] == 0xffffffffu;
-                        const uint32_t tag = (uint32_t)(((c * 2 + (e0 >> 6)) << 6) + lane);
+                        const uint32_t tag = (uint32_t)((t << 6) + lane);
                         if (freeh) T2[h] = tag;
                         wave_lds_sync();
                         const bool win = freeh && T2[h] == tag;
@@ -1120,16 +1155,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                 const double4 *gbuf = buf + g0 + nb - 64;  // bit position p <-> gbuf[63 - p]
                 const int nit = __builtin_amdgcn_readfirstlane(wave_max_i(__builtin_popcountll(m)));
                 if constexpr (KEYS && MODE != kModeRadius) {
-                    // key lists: 8 candidates per lane at a time into one merge network
-                    // (insert_keys8); iterations past nit find m = 0 everywhere (+inf keys).
+                    // key lists: NB candidates per lane at a time into one merge network
+                    // (insert_keys); iterations past nit find m = 0 everywhere (+inf keys).
                     // No exact threshold test: a key past the list's end drops out, and every
                     // candidate sharing the k-th key's truncation reaches the (k+1)-th slot
                     // (the near-tie check)
-                    for (int it = 0; it < nit; it += 8) {
-                        n_acc += (uint32_t)min(8, nit - it);
-                        double nk[8];
+                    constexpr int NB = key_batch<KMAX>();
+                    for (int it = 0; it < nit; it += NB) {
+                        n_acc += (uint32_t)min(NB, nit - it);
+                        double nk[NB];
 #pragma unroll
-                        for (int j = 0; j < 8; ++j) {
+                        for (int j = 0; j < NB; ++j) {
                             const bool has = m != 0ull;
                             const int lz = __builtin_clzll(m | 1ull);
                             m &= ~(0x8000000000000000ull >> lz);
@@ -1138,7 +1174,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                             const double e2 = (dx * dx + dy * dy) + dz * dz;
                             nk[j] = make_key(has, e2, (uint32_t)__double_as_longlong(c.w), a.smask);
                         }
-                        insert_keys8<KMAX>(bd, nk);
+                        insert_keys<KMAX, NB>(bd, nk);
                     }
                 } else for (int it = 0; it < nit; ++it) {
                     // branch-free body (lanes without bits read a valid stale slot and insert inf)
@@ -1917,7 +1953,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                 ps_inv.add(m, k, iv);
                 ps_d.add(m, k, dv);
             }
-            stamp(t_seed);  // stamp builds: pass 1 of the key-list epilogue (no seeds above 8 slots)
+            stamp(t_epi);  // stamp builds: pass 1 of the key-list epilogue
             if (__builtin_amdgcn_ballot_w64(amb || !ok) != 0) {
                 list_tile();
                 return;
@@ -2018,7 +2054,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                 }
                 ps.add(m, k, w);
             }
-            stamp(t_seed);  // stamp builds: pass 1 of the key-list epilogue (no seeds above 8 slots)
+            stamp(t_epi);  // stamp builds: pass 1 of the key-list epilogue
             if (__builtin_amdgcn_ballot_w64(amb || !ok) != 0) {
                 list_tile();
                 return;
