@@ -115,6 +115,22 @@ def rbf_resolved(args):
     return kern, eps, deg, m
 
 
+def rbf_kernel_label(kern, k, m, deg):
+    """The solver launch_rbf (ptv_rbf.hip) picks: k_rbf_spd16 for the SPD kernels without a
+    polynomial (M <= 32), the null-space k_rbf_ns for the scale-invariant kernels with degree >= their
+    minimum (1, 4 or 10 monomials, k <= 32; 10 only for k <= 24), else the pivoting k_rbf_local."""
+    M = (m + 7) & ~7
+    npoly = m - k
+    if kern in ("gaussian", "inverse_multiquadric", "inverse_quadratic") and m == k and M <= 32:
+        return f"k_rbf_spd16<{M}>"
+    min_deg = {"linear": 0, "thin_plate_spline": 1, "cubic": 1, "quintic": 2}
+    if (kern in min_deg and deg >= min_deg[kern] and npoly in (1, 4, 10) and npoly < k <= 32
+            and (npoly < 10 or k <= 24)):
+        nc = 16 if k <= 16 else 20 if k <= 20 else 24 if k <= 24 else 32
+        return f"k_rbf_ns<{nc}, {npoly}>"
+    return f"k_rbf_local<{M}>" if M <= 64 else "k_rbf_big"
+
+
 def rbf_flops_per_voxel(k, m):
     """distances 8 k(k-1)/2, LU (2/3) m^3, substitution + build 6 m^2, eval 8k + 6m."""
     return 8 * k * (k - 1) / 2 + (2.0 / 3.0) * m ** 3 + 6 * m ** 2 + 8 * k + 6 * m
@@ -666,10 +682,7 @@ def main_interp(args):
         tf = flops / (avg["ms_solve"] * 1e-3) / 1e12
         roof = {"bound": "fp64", "achieved": round(tf, 2), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(tf / FP64_PEAK_TFLOPS, 4), "traffic": None,
-                # the launcher's choice (ptv_rbf.hip rbf_spd): SPD kernels without a polynomial, M <= 32
-                "kernel": (f"k_rbf_spd16<{(m_sys + 7) & ~7}>"
-                           if args.rbf_kernel in ("gaussian", "inverse_multiquadric", "inverse_quadratic")
-                           and m_sys == k and (m_sys + 7) & ~7 <= 32 else f"k_rbf_local<{(m_sys + 7) & ~7}>"),
+                "kernel": rbf_kernel_label(kern, k, m_sys, deg),
                 "alg_flops_per_launch": flops, "kernel_ms": round(avg["ms_solve"], 3),
                 "knn_slots_ms": round(avg["ms_knn"], 3)}
     else:

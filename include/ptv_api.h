@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define PTV_API_VERSION 8
+#define PTV_API_VERSION 9
 
 /* error codes */
 #define PTV_OK 0
@@ -64,6 +64,9 @@ extern "C" {
 /* local RBF, diagnostics: SPD systems through the LDS-broadcast kernel (k_rbf_spd, the one the
  * register kernel's out-of-range-pivot rerun uses) instead of k_rbf_spd16 (ABI v8) */
 #define PTV_FLAG_RBF_SPD_LDS 4u
+/* local RBF, diagnostics: the scale-invariant kernels through the partial-pivoting solver
+ * (k_rbf_local) instead of the null-space solver k_rbf_ns (ABI v9) */
+#define PTV_FLAG_RBF_PIVOTING 8u
 
 typedef struct ptv_ctx ptv_ctx;
 
@@ -158,6 +161,9 @@ typedef struct {
     double ms_cull;      /* slab_halo cull + exactness check (inside ms_bin / before ms_knn) */
     int64_t n_repair_tiles; /* k >= 13: 4x4x4 tiles rerun with exact (d2, slot) lists because two
                              * distinct distances shared a packed key's truncation (ABI v8) */
+    int64_t n_rbf_pivoted;  /* local RBF, scale-invariant kernels: voxels the null-space solver handed
+                             * to the partial-pivoting solver (rank-deficient polynomial block, a
+                             * non-positive pivot, ...; ABI v9) */
 } ptv_stats;
 
 /*

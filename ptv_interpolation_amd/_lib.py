@@ -84,6 +84,7 @@ F64 = 0
 F32 = 1
 FLAG_OUT_F32 = 2  # U, V, W written as float32 (main.py:230 astype, fused)
 FLAG_RBF_SPD_LDS = 4  # local RBF diagnostics: SPD systems through the LDS-broadcast kernel
+FLAG_RBF_PIVOTING = 8  # local RBF diagnostics: scale-invariant kernels through the pivoting solver
 
 
 class DivParams(C.Structure):
@@ -120,7 +121,8 @@ class Stats(C.Structure):
                 ("n_cells", C.c_int64), ("cells", C.c_int32 * 3), ("cell_size", C.c_double * 3),
                 ("r0", C.c_double), ("ms_solve", C.c_double), ("n_singular", C.c_int64),
                 ("ms_stencil", C.c_double), ("n_binned", C.c_int64), ("halo_required", C.c_double),
-                ("ms_cull", C.c_double), ("n_repair_tiles", C.c_int64)]
+                ("ms_cull", C.c_double), ("n_repair_tiles", C.c_int64),
+                ("n_rbf_pivoted", C.c_int64)]
 
     def as_dict(self):
         d = {f: getattr(self, f) for f, _ in self._fields_}

@@ -22,11 +22,12 @@ BUILD = os.path.join(HERE, "csrc", "_build")
 # the k-NN kernel's list lengths compile in parallel (ptv_knn_k*.hip instantiate ptv_knn_impl.hpp)
 KNN_PARTS = ["ptv_knn_k" + g + ".hip" for g in "abcdefgh"]
 SOURCES = (["ptv_api.cpp", "ptv_bin.hip", "ptv_knn.hip"] + KNN_PARTS +
-           ["ptv_rbf.hip", "ptv_div.hip", "ptv_mask.hip", "ptv_filter.hip", "ptv_linear.hip"])
+           ["ptv_rbf.hip"] + ["ptv_rbf_ns_" + g + ".hip" for g in "abcd"] +
+           ["ptv_div.hip", "ptv_mask.hip", "ptv_filter.hip", "ptv_linear.hip"])
 ARCH = os.environ.get("PTV_OFFLOAD_ARCH", "gfx950")
 # per-file extras: the local-RBF kernel keeps each voxel's system row in registers, so every
 # loop over the row must unroll fully (a partial unroll turns the row into scratch memory)
-EXTRA = {"ptv_rbf.hip": ["-mllvm", "-pragma-unroll-threshold=1000000"]}
+EXTRA = {f: ["-mllvm", "-pragma-unroll-threshold=1000000"] for f in ["ptv_rbf.hip"] + ["ptv_rbf_ns_" + g + ".hip" for g in "abcd"]}
 
 COMMON = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", f"--offload-arch={ARCH}",
           "-I", INCLUDE, "-I", CSRC, "-Wno-unused-result"]

@@ -74,6 +74,7 @@ struct ptv_ctx {
     DevBuf<int> lat_order[kMaxLattice];                          // longest-first block order per level
     DevBuf<uint32_t> slots;                                      // local RBF: chunk k-NN slots
     DevBuf<int> rbf_pw, rbf_status;                              // monomial exponents, singular count
+    DevBuf<uint32_t> rbf_nslist;                                 // local RBF: voxels k_rbf_ns hands over
     DevBuf<double> smooth;                                       // per-particle smoothing (host calls)
     DevBuf<uint8_t> fld[4];                                      // divergence host calls: U, V, W, out
     DevBuf<double> mask_axes;                                    // sample_mask: raw axes (ascending)
@@ -219,6 +220,7 @@ int ptv_free(ptv_ctx *c) {
     c->slots.release();
     c->rbf_pw.release();
     c->rbf_status.release();
+    c->rbf_nslist.release();
     c->lin_simp.release();
     c->lin_nbr.release();
     c->lin_v2s.release();
@@ -786,10 +788,11 @@ int run_rbf(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_rbf
     PTV_TRY(prepare(c, p, g, &sp, ax, ay, az, qx, qy, qz, s, kl, b));
     const std::vector<int> pw = monomial_powers(prm->degree);
     PTV_TRY(c->rbf_pw.ensure(pw.size() + 1));
-    PTV_TRY(c->rbf_status.ensure(3));
+    PTV_TRY(c->rbf_status.ensure(6));
+    PTV_TRY(c->rbf_nslist.ensure(kRbfNsCap));
     if (!pw.empty())
         PTV_HIP(hipMemcpyAsync(c->rbf_pw.p, pw.data(), pw.size() * sizeof(int), hipMemcpyHostToDevice, s));
-    const int st_init[3] = {0, 0x7fffffff, 0};
+    const int st_init[6] = {0, 0x7fffffff, 0, 0, 0, 0};
 
     const int64_t plane = g->nx * g->ny;
     const int64_t z0 = g->z_begin, z1 = g->z_end;
@@ -818,11 +821,15 @@ int run_rbf(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_rbf
     ra.epsilon = prm->epsilon;
     ra.smoothing = prm->smoothing;
     ra.flags = prm->flags;
-    int st_out[3] = {0, 0, 0};
+    int st_out[6] = {0, 0, 0, 0, 0, 0};
+    bool ns_overflow = false;  // pass 0's null-space list overflowed: pass 1 pivots every voxel
     for (int pass = 0; pass < 2; ++pass) {
-    // pass 1 (rare): k_rbf_spd16 met a pivot its reciprocal does not serve; redo every chunk with
-    // the LDS-broadcast SPD kernel (same arithmetic plus the IEEE division for such pivots)
+    // pass 1 (rare): k_rbf_spd16 met a pivot its reciprocal does not serve, or k_rbf_ns flagged more
+    // voxels in a chunk than its list holds; redo every chunk with the LDS-broadcast SPD kernel (same
+    // arithmetic plus the IEEE division for such pivots) and without the null-space kernel
     ra.spd_lds = pass;
+    ra.ns_list = pass == 0 ? c->rbf_nslist.p : nullptr;
+    ra.ns_cap = kRbfNsCap;
     PTV_HIP(hipMemcpyAsync(c->rbf_status.p, st_init, sizeof(st_init), hipMemcpyHostToDevice, s));
     for (int ch = 0; ch < nchunks; ++ch) {
         const int za = (int)(z0 + (int64_t)ch * cp), zb = (int)std::min<int64_t>(z1, za + cp);
@@ -843,11 +850,14 @@ int run_rbf(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_rbf
     }
     PTV_HIP(hipMemcpyAsync(st_out, c->rbf_status.p, sizeof(st_out), hipMemcpyDeviceToHost, s));
     PTV_HIP(hipStreamSynchronize(s));
-    if (st_out[2] == 0) break;
+    if (st_out[2] == 0 && st_out[4] == 0) break;
+    ns_overflow = st_out[4] != 0;
     }
     c->rbf_chunks = nchunks;
     *n_singular = st_out[0];
     c->last.n_singular = st_out[0];
+    // voxels solved by the pivoting kernel after k_rbf_ns flagged them (every voxel of a rerun pass)
+    c->last.n_rbf_pivoted = ns_overflow ? (z1 - z0) * plane : st_out[5];
     if (st_out[0] > 0) {
         set_error("Singular matrix. (" + std::to_string(st_out[0]) + " voxel system(s), first at linear voxel " +
                   std::to_string(st_out[1]) + ")");

@@ -163,6 +163,7 @@ int launch_linear_brute(const LinearKernelArgs &a, int nflag, const double *ax, 
                         hipStream_t s);
 
 // ---- local RBF (ptv_rbf.hip) ----
+constexpr int kRbfNsCap = 1 << 14;   // voxels per launch k_rbf_ns may hand to the pivoting kernel
 constexpr int kRbfMaxSystem = 128;  // k + #monomials per voxel system (> 64: k_rbf_big, LDS-resident)
 
 struct RbfKernelArgs {
@@ -177,14 +178,37 @@ struct RbfKernelArgs {
     uint32_t flags;
     int spd_lds;       // SPD systems: the LDS-broadcast k_rbf_spd instead of k_rbf_spd16 (the
                        // rerun after k_rbf_spd16 flagged an out-of-range pivot in status[2])
+    // null-space kernel (ptv_rbf_ns.hpp): chunk-local voxels it hands to the pivoting kernel
+    uint32_t *ns_list; // NULL: the null-space path is off for this launch
+    int ns_cap;        // entries of ns_list
+    // pivoting kernel in list mode: solve only the voxels vlist[0 .. min(*vcount, ns_cap))
+    const uint32_t *vlist;
+    const int *vcount;
+    unsigned long long *stamps;  // dev builds (PTV_NS_STAMP): per-wave phase cycles of k_rbf_ns, 8 per wave
+    long long stamp_cap;
 };
+
+// null-space local-RBF kernels k_rbf_ns<NC, NP> (ptv_rbf_ns.hpp), one translation unit per
+// row-slot count NC (16, 20, 24, 32); np = number of monomials (1, 4 or 10)
+#define PTV_RBF_NS_DECL(NC)                                                                                   \
+    void launch_rbf_ns##NC(const RbfKernelArgs &ka, long long nvox, int np, hipStream_t s, const double4 *prec, \
+                           const double4 *pval, const uint32_t *slots, const double *ax, const double *ay,       \
+                           const double *az, const double *qx, const double *qy, const double *qz,               \
+                           const double *smooth, const int *pw, const uint8_t *mask, double *U, double *V,      \
+                           double *W, int *status)
+PTV_RBF_NS_DECL(16);
+PTV_RBF_NS_DECL(20);
+PTV_RBF_NS_DECL(24);
+PTV_RBF_NS_DECL(32);
 
 int rbf_system_size(int m);  // padded system size served, 0 if unsupported
 
 // slots: (z1 - z0, ny, nx, k) neighbour slots from launch_knn(kModeSlots); pw: the
 // monomial exponents (m - k entries, px | py << 8 | pz << 16); status[0] counts singular
 // systems, status[1] keeps the lowest singular voxel index, status[2] != 0 asks for a rerun
-// with spd_lds set.
+// with spd_lds set; the null-space path counts its flagged voxels of this launch in status[3]
+// (reset by launch_rbf), sets status[4] when more than ns_cap were flagged (the host then reruns
+// without it) and accumulates the flagged voxels of every launch in status[5].
 int launch_rbf(const RbfKernelArgs &ka, const Binned &b, const uint32_t *slots, const double *ax, const double *ay,
                const double *az, const double *qx, const double *qy, const double *qz, const double *smooth,
                const int *pw, const uint8_t *mask, double *U, double *V, double *W, int *status, hipStream_t s);

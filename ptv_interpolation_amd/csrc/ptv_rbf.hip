@@ -36,226 +36,16 @@
 // reference to the conditioning of the system (see tests/test_gpu_rbf.py and DESIGN.md).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
 #include <cstdlib>
 
 #include "../../include/ptv_api.h"
 #include "ptv_kernels.hpp"
+#include "ptv_rbf_math.hpp"
 
 namespace ptv {
-
-// 1/p from v_rcp_f64 and two Newton steps (within an ulp of the IEEE quotient; the
-// elimination multiplier l = a * (1/p) is LAPACK dgetf2's reciprocal scaling anyway).
-// Valid only where 1/p is a normal number: see elim_multiplier.
-__device__ __forceinline__ double rcp_nr(double p) {
-    double r = __builtin_amdgcn_rcp(p);
-    double e = fma(-p, r, 1.0);
-    r = fma(r, e, r);
-    e = fma(-p, r, 1.0);
-    return fma(r, e, r);
-}
-
-// l = a / p as LAPACK dgetf2 forms it: a * (1/p) when |p| >= sfmin (DBL_MIN), a / p below.
-// The Newton reciprocal serves 2^-1020 < |p| < 2^1020; outside it (an infinite pivot gives
-// rcp 0 and fma(-inf, 0, 1) = NaN; a subnormal one overflows the seed) the IEEE forms run.
-__device__ __forceinline__ double elim_multiplier(double a, double p) {
-    const double ap = fabs(p);
-    if (ap > 0x1p-1020 && ap < 0x1p1020) return a * rcp_nr(p);
-    return ap >= DBL_MIN ? a * (1.0 / p) : a / p;
-}
-
-// 1/p for the SPD kernels' multipliers l = a * (1/p) (LAPACK dgetf2's reciprocal scaling),
-// branch-free: the Newton reciprocal where it is valid, IEEE division otherwise (an infinite or
-// subnormal pivot; a branch here made the 16-lane kernel's unrolled elimination spill)
-__device__ __forceinline__ double spd_recip(double p) {
-    const double ap = fabs(p);
-    const double q = 1.0 / p;
-    const double r = rcp_nr(p);
-    return (ap > 0x1p-1020 && ap < 0x1p1020) ? r : q;
-}
-
-__device__ __forceinline__ void rbf_wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// exp(x) for x <= 0, bit-identical to the device libm (ocml) exp this kernel used before: the
-// same reduction (x log2 e rounded to even, Cody-Waite ln 2 in two parts), degree-11 polynomial
-// in Horner form, ldexp and underflow to 0 below -1075.  Written out so that every Horner step is
-// one VOP3 v_fma_f64 with its coefficient in an SGPR pair: the compiler's form kept the
-// coefficients in VGPRs and paid a v_mov_b64 per step (v_fmac overwrites its addend).
-__device__ __forceinline__ double horner(double r, double p, double c) {
-    double o;
-    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(o) : "v"(r), "v"(p), "s"(c));
-    return o;
-}
-__device__ __forceinline__ double exp_nonpos(double x) {
-    const double dn = __builtin_rint(x * 0x1.71547652b82fep+0);
-    double r = fma(-0x1.62e42fefa39efp-1, dn, x);
-    r = fma(-0x1.abc9e3b39803fp-56, dn, r);
-    double p = fma(0x1.ade156a5dcb37p-26, r, 0x1.28af3fca7ab0cp-22);
-    p = horner(r, p, 0x1.71dee623fde64p-19);
-    p = horner(r, p, 0x1.a01997c89e6b0p-16);
-    p = horner(r, p, 0x1.a01a014761f6ep-13);
-    p = horner(r, p, 0x1.6c16c1852b7b0p-10);
-    p = horner(r, p, 0x1.1111111122322p-7);
-    p = horner(r, p, 0x1.55555555502a1p-5);
-    p = horner(r, p, 0x1.5555555555511p-3);
-    p = horner(r, p, 0x1.000000000000bp-1);
-    p = fma(r, p, 1.0);
-    p = fma(r, p, 1.0);
-    const double e = __builtin_amdgcn_ldexp(p, (int)dn);
-    return -1075.0 > x ? 0.0 : e;
-}
-
-// IEEE sqrt for x >= 2^-767 (the LLVM gfx9 f64 expansion without its small-input rescale),
-// branch-free; +-0 and +inf are returned as they are.  For 0 < x < 2^-767 it may differ from
-// sqrt() in the last bit, which no SPD kernel can see: phi(r) of the gaussian, inverse
-// multiquadric and inverse quadratic kernels only uses r * r + 1 or exp(-r * r).
-__device__ __forceinline__ double sqrt_spd(double x) {
-    const double y = __builtin_amdgcn_rsq(x);
-    double g = x * y, h = y * 0.5;
-    const double r = fma(-h, g, 0.5);
-    g = fma(g, r, g);
-    h = fma(h, r, h);
-    g = fma(fma(-g, g, x), h, g);
-    g = fma(fma(-g, g, x), h, g);
-    return __builtin_amdgcn_class(x, 0x260) ? x : g;  // +inf, +0, -0
-}
-
-// scipy/interpolate/_rbfinterp_pythran.py kernel functions (r >= 0)
-template <int KERN>
-__device__ __forceinline__ double rbf_phi(double r) {
-    if constexpr (KERN == PTV_RBF_LINEAR) return -r;
-    if constexpr (KERN == PTV_RBF_THIN_PLATE_SPLINE) return r == 0.0 ? 0.0 : (r * r) * log(r);
-    if constexpr (KERN == PTV_RBF_CUBIC) return (r * r) * r;
-    if constexpr (KERN == PTV_RBF_QUINTIC) return -((((r * r) * r) * r) * r);
-    if constexpr (KERN == PTV_RBF_MULTIQUADRIC) return -sqrt(r * r + 1.0);
-    if constexpr (KERN == PTV_RBF_INVERSE_MULTIQUADRIC) return 1.0 / sqrt(r * r + 1.0);
-    if constexpr (KERN == PTV_RBF_INVERSE_QUADRATIC) return 1.0 / (r * r + 1.0);
-    if constexpr (KERN == PTV_RBF_GAUSSIAN) return exp_nonpos(-(r * r));
-    return 0.0;
-}
-
-__device__ double rbf_phi_rt(int kern, double r) {
-    switch (kern) {
-        case PTV_RBF_LINEAR: return rbf_phi<PTV_RBF_LINEAR>(r);
-        case PTV_RBF_THIN_PLATE_SPLINE: return rbf_phi<PTV_RBF_THIN_PLATE_SPLINE>(r);
-        case PTV_RBF_CUBIC: return rbf_phi<PTV_RBF_CUBIC>(r);
-        case PTV_RBF_QUINTIC: return rbf_phi<PTV_RBF_QUINTIC>(r);
-        case PTV_RBF_MULTIQUADRIC: return rbf_phi<PTV_RBF_MULTIQUADRIC>(r);
-        case PTV_RBF_INVERSE_MULTIQUADRIC: return rbf_phi<PTV_RBF_INVERSE_MULTIQUADRIC>(r);
-        case PTV_RBF_INVERSE_QUADRATIC: return rbf_phi<PTV_RBF_INVERSE_QUADRATIC>(r);
-        default: return rbf_phi<PTV_RBF_GAUSSIAN>(r);
-    }
-}
-
-// libm pow for the rare exponents > 3 (degree >= 4); out of line so its code exists once
-__device__ __noinline__ double ipow_slow(double x, int p) { return pow(x, (double)p); }
-
-// x ** p for the small integer monomial exponents (np.prod(x ** powers[j]))
-__device__ __forceinline__ double ipow(double x, int p) {
-    if (p == 0) return 1.0;
-    if (p == 1) return x;
-    if (p == 2) return x * x;
-    if (p == 3) return (x * x) * x;
-    return ipow_slow(x, p);
-}
-
-// monomial with exponents packed as px | py << 8 | pz << 16
-__device__ __forceinline__ double mono(double hx, double hy, double hz, int code) {
-    return (ipow(hx, code & 255) * ipow(hy, (code >> 8) & 255)) * ipow(hz, code >> 16);
-}
-
-// ---- segment reductions in registers: DPP within 16-lane rows (quad_perm xor 1, xor 2,
-// row_half_mirror, row_mirror), v_permlane16_swap / v_permlane32_swap (gfx950) across rows.
-// Every lane of the segment ends with the same value (each step combines symmetric pairs). ----
-template <int CTRL>
-__device__ __forceinline__ unsigned dpp_u32(unsigned v) {
-    // bound_ctrl: every source lane of these patterns is valid, so no old value is needed
-    // (the compiler then drops the v_mov that would initialise it)
-    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, true);
-}
-template <int CTRL>
-__device__ __forceinline__ double dpp_f64(double v) {
-    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-    const unsigned lo = dpp_u32<CTRL>((unsigned)b), hi = dpp_u32<CTRL>((unsigned)(b >> 32));
-    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-}
-// (v of this lane's row partner, v of its half-wave partner): the two results of a swap of v with itself
-template <int W>
-__device__ __forceinline__ void swap_self(unsigned v, unsigned &a, unsigned &b) {
-    if constexpr (W == 16) {
-        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-        a = r[0];
-        b = r[1];
-    } else {
-        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-        a = r[0];
-        b = r[1];
-    }
-}
-template <int W>
-__device__ __forceinline__ void swap_self_f64(double v, double &a, double &b) {
-    const unsigned long long x = (unsigned long long)__double_as_longlong(v);
-    unsigned al, bl, ah, bh;
-    swap_self<W>((unsigned)x, al, bl);
-    swap_self<W>((unsigned)(x >> 32), ah, bh);
-    a = __longlong_as_double((long long)(((unsigned long long)ah << 32) | al));
-    b = __longlong_as_double((long long)(((unsigned long long)bh << 32) | bl));
-}
-
-template <int L, typename Op>
-__device__ __forceinline__ double seg_reduce(double v, Op op) {
-    static_assert(L == 16 || L == 32 || L == 64, "segment width");
-    v = op(v, dpp_f64<0xB1>(v));   // quad_perm [1,0,3,2]
-    v = op(v, dpp_f64<0x4E>(v));   // quad_perm [2,3,0,1]
-    v = op(v, dpp_f64<0x141>(v));  // row_half_mirror
-    v = op(v, dpp_f64<0x140>(v));  // row_mirror
-    if constexpr (L >= 32) {
-        double a, b;
-        swap_self_f64<16>(v, a, b);
-        v = op(a, b);
-    }
-    if constexpr (L == 64) {
-        double a, b;
-        swap_self_f64<32>(v, a, b);
-        v = op(a, b);
-    }
-    return v;
-}
-template <int L>
-__device__ __forceinline__ unsigned seg_max_u32(unsigned v) {
-    v = max(v, dpp_u32<0xB1>(v));
-    v = max(v, dpp_u32<0x4E>(v));
-    v = max(v, dpp_u32<0x141>(v));
-    v = max(v, dpp_u32<0x140>(v));
-    if constexpr (L >= 32) {
-        unsigned a, b;
-        swap_self<16>(v, a, b);
-        v = max(a, b);
-    }
-    if constexpr (L == 64) {
-        unsigned a, b;
-        swap_self<32>(v, a, b);
-        v = max(a, b);
-    }
-    return v;
-}
-template <int L>
-__device__ __forceinline__ double seg_sum(double v) {
-    return seg_reduce<L>(v, [](double x, double y) { return x + y; });
-}
-template <int L>
-__device__ __forceinline__ double seg_min(double v) {
-    return seg_reduce<L>(v, [](double x, double y) { return fmin(x, y); });
-}
-template <int L>
-__device__ __forceinline__ double seg_max(double v) {
-    return seg_reduce<L>(v, [](double x, double y) { return fmax(x, y); });
-}
 
 // Entries j in [j0, j0 + n) of system row li, into the lane's column of the per-wave LDS
 // scratch (sc[jj * 64 + lane]).  A rolled loop: the phi / monomial code is emitted once, so
@@ -321,8 +111,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M <= 32 ? 3
 
     const long long plane = (long long)a.nx * a.ny;
     const long long nvox = (long long)(a.z1 - a.z0) * plane;
-    const long long v = ((long long)blockIdx.x * 4 + wid) * SPW + seg;  // chunk-local voxel
-    const bool valid = v < nvox;
+    long long v = ((long long)blockIdx.x * 4 + wid) * SPW + seg;  // chunk-local voxel
+    bool valid = v < nvox;
+    if (a.vlist != nullptr) {  // list mode: the voxels k_rbf_ns handed over (count on the device)
+        const long long n = min((long long)*a.vcount, (long long)a.ns_cap);
+        valid = v < n;
+        v = valid ? (long long)a.vlist[v] : 0;
+    }
     const long long vc = valid ? v : nvox - 1;
     const int iz = a.z0 + (int)(vc / plane);
     const long long rem = vc % plane;
@@ -961,33 +756,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PTV_RBF_SPD
 // one 8-cycle ds_read_b128 per two pivot-row values).  Same arithmetic and order as k_rbf_spd
 // (no pivoting, fma updates, the multiplier a * spd_recip(p)), so the two agree bit for bit.
 // ---------------------------------------------------------------------------
-template <int N>
-__device__ __forceinline__ double rowbcast(double v) {  // lane N of this lane's 16-lane row
-    return __longlong_as_double(
-        __builtin_amdgcn_update_dpp(0LL, __double_as_longlong(v), 0x150 + N, 0xF, 0xF, true));
-}
-
-// the same with a lane index that the unrolled loops fold to a constant (the DPP control must be one)
-__device__ __forceinline__ double rowbcast_n(int n, double v) {
-    switch (n & 15) {
-        case 0: return rowbcast<0>(v);
-        case 1: return rowbcast<1>(v);
-        case 2: return rowbcast<2>(v);
-        case 3: return rowbcast<3>(v);
-        case 4: return rowbcast<4>(v);
-        case 5: return rowbcast<5>(v);
-        case 6: return rowbcast<6>(v);
-        case 7: return rowbcast<7>(v);
-        case 8: return rowbcast<8>(v);
-        case 9: return rowbcast<9>(v);
-        case 10: return rowbcast<10>(v);
-        case 11: return rowbcast<11>(v);
-        case 12: return rowbcast<12>(v);
-        case 13: return rowbcast<13>(v);
-        case 14: return rowbcast<14>(v);
-        default: return rowbcast<15>(v);
-    }
-}
 
 
 template <int M, int KERN>
@@ -1303,6 +1071,30 @@ static bool rbf_spd(const RbfKernelArgs &ka, const double *smooth) {
     return pd_kernel && ka.m == ka.k && smooth == nullptr && ka.smoothing >= 0.0 && rbf_system_size(ka.m) <= 32;
 }
 
+// whether k_rbf_ns (ptv_rbf_ns.hpp) serves the launch: a scale-invariant conditionally positive
+// definite kernel (the kernels interpolate_field can reach, interpolator.py:162-167: no epsilon
+// there) with degree >= its order - 1 (then (Q^T Phi Q)[r:, r:] is positive definite), 1, 4 or
+// 10 monomials, k <= 32 row slots (10 monomials: k <= 24, registers).  The scale-dependent
+// kernels stay on the pivoting kernel: for the flat gaussian eps = 0.3 systems (cond 6e8) the
+// projected system lost 20x LAPACK's accuracy (tools/rbf_nullspace_proto.py).
+static bool rbf_ns(const RbfKernelArgs &ka, const double *smooth, long long nvox) {
+    if (const char *e = dev_knob("PTV_RBF_NS"))  // dev knob: 0 = the pivoting kernel throughout
+        if (e[0] == '0') return false;
+    if (ka.ns_list == nullptr || ka.ns_cap <= 0 || nvox > 0xffffffffLL || (ka.flags & PTV_FLAG_RBF_PIVOTING)) return false;
+    const int np = ka.m - ka.k;
+    if (!(np == 1 || np == 4 || (np == 10 && ka.k <= 24))) return false;
+    if (ka.k <= np || ka.k > 32) return false;
+    if (smooth == nullptr && !(ka.smoothing >= 0.0)) return false;
+    const int degree = np == 1 ? 0 : (np == 4 ? 1 : 2);
+    switch (ka.kernel) {
+        case PTV_RBF_LINEAR: return degree >= 0;             // -r: order 1
+        case PTV_RBF_THIN_PLATE_SPLINE: return degree >= 1;  // r^2 log r: order 2
+        case PTV_RBF_CUBIC: return degree >= 1;              // r^3: order 2
+        case PTV_RBF_QUINTIC: return degree >= 2;            // -r^5: order 3
+        default: return false;
+    }
+}
+
 int rbf_system_size(int m) {
     if (m < 1 || m > kRbfMaxSystem) return 0;
     return m <= 64 ? (m + 7) & ~7 : m;  // k_rbf_local pads to a multiple of 8; k_rbf_big takes m
@@ -1338,12 +1130,26 @@ int launch_rbf(const RbfKernelArgs &ka, const Binned &b, const uint32_t *slots, 
         return PTV_E_ARG;
     }
     if (M > 64) {
+        // one 64-lane block per voxel: sub-launches of whole planes, at most 2^26 voxels (2^32 work
+        // items) each, with the slots of each sub-launch's first plane
+        const long long plane = (long long)ka.nx * ka.ny;
+        if (plane > (1LL << 26)) {
+            set_error("local RBF: grid plane too large for the m > 64 kernel");
+            return PTV_E_UNSUPPORTED;
+        }
         const size_t bytes = rbf_big_lds_bytes(ka.m);
         PTV_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_rbf_big),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
-        hipLaunchKernelGGL(k_rbf_big, dim3((unsigned)nvox), dim3(64), bytes, s, ka, b.prec, b.pval, slots, ax, ay, az,
-                           qx, qy, qz, smooth, pw, mask, U, V, W, status);
-        PTV_HIP(hipGetLastError());
+        const int step = (int)std::max<long long>(1, (1LL << 26) / plane);
+        for (int za = ka.z0; za < ka.z1; za += step) {
+            RbfKernelArgs sa = ka;
+            sa.z0 = za;
+            sa.z1 = std::min(ka.z1, za + step);
+            const uint32_t *sl = slots + (size_t)(za - ka.z0) * plane * ka.k;
+            hipLaunchKernelGGL(k_rbf_big, dim3((unsigned)((long long)(sa.z1 - sa.z0) * plane)), dim3(64), bytes, s, sa,
+                               b.prec, b.pval, sl, ax, ay, az, qx, qy, qz, smooth, pw, mask, U, V, W, status);
+            PTV_HIP(hipGetLastError());
+        }
         return PTV_OK;
     }
     if (rbf_spd(ka, smooth)) {
@@ -1378,9 +1184,34 @@ int launch_rbf(const RbfKernelArgs &ka, const Binned &b, const uint32_t *slots, 
         PTV_HIP(hipGetLastError());
         return PTV_OK;
     }
+    RbfKernelArgs pa = ka;
+    long long pn = nvox;
+    if (rbf_ns(ka, smooth, nvox)) {
+        PTV_HIP(hipMemsetAsync(status + 3, 0, sizeof(int), s));
+        RbfKernelArgs na = ka;
+        na.stamps = g_dbg;  // diagnostics: only PTV_NS_STAMP builds write them
+        na.stamp_cap = g_dbg_cap;
+        const int np = ka.m - ka.k;
+        if (ka.k <= 16)
+            launch_rbf_ns16(na, nvox, np, s, b.prec, b.pval, slots, ax, ay, az, qx, qy, qz, smooth, pw, mask, U, V, W, status);
+        else if (ka.k <= 20)
+            launch_rbf_ns20(na, nvox, np, s, b.prec, b.pval, slots, ax, ay, az, qx, qy, qz, smooth, pw, mask, U, V, W, status);
+        else if (ka.k <= 24)
+            launch_rbf_ns24(na, nvox, np, s, b.prec, b.pval, slots, ax, ay, az, qx, qy, qz, smooth, pw, mask, U, V, W, status);
+        else
+            launch_rbf_ns32(na, nvox, np, s, b.prec, b.pval, slots, ax, ay, az, qx, qy, qz, smooth, pw, mask, U, V, W, status);
+        PTV_HIP(hipGetLastError());
+        // the voxels it flagged: the pivoting kernel over the list (grid sized for ns_cap; waves past the
+        // device count exit at once)
+        pa.vlist = ka.ns_list;
+        pa.vcount = status + 3;
+        pn = ka.ns_cap;
+    } else {
+        pa.vlist = nullptr;
+    }
     switch (M) {
 #define PTV_RCASE(X) \
-    case X: launch_rbf_t<X>(ka, nvox, s, b.prec, b.pval, slots, ax, ay, az, qx, qy, qz, smooth, pw, mask, U, V, W, status); break;
+    case X: launch_rbf_t<X>(pa, pn, s, b.prec, b.pval, slots, ax, ay, az, qx, qy, qz, smooth, pw, mask, U, V, W, status); break;
         PTV_RCASE(8)
         PTV_RCASE(16)
         PTV_RCASE(24)

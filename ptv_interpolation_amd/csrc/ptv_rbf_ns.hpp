@@ -1,0 +1,553 @@
+// ptv_rbf_ns.hpp — local RBF by the null-space method (gfx950): the per-voxel saddle-point
+// systems of the reference-reachable kernels (thin-plate spline, cubic, quintic, linear) and of
+// every other kernel with a polynomial tail, solved with a STATIC elimination order.
+//
+// The system scipy builds per voxel (RBFInterpolator(neighbors=k), _rbfinterp.py:82-127, called
+// from interpolator.py:162-167) is
+//     [Phi  P] [c]   [d]        Phi = phi(eps |y_i - y_j|) + s_i delta_ij   (k x k, symmetric)
+//     [P^T  0] [e] = [0]        P   = monomials of yhat                      (k x r, r = 1, 4, 10)
+// and scipy factors it with LAPACK dgesv (partial pivoting).  Partial pivoting needs a
+// data-dependent pivot row, and a 16-lane segment can only broadcast a COMPILE-TIME lane in
+// registers (v_mov_b64_dpp row_newbcast): the pivoting kernel k_rbf_local pays an LDS round trip
+// and two wave syncs per column for it (0.02-0.03 of FP64 peak).  For a
+// conditionally positive definite kernel of order o with degree >= o - 1 (linear, multiquadric:
+// o = 1; thin-plate spline, cubic: o = 2; quintic: o = 3; the positive definite gaussian /
+// inverse multiquadric / inverse quadratic: o = 0) the same solution is, exactly in real
+// arithmetic:
+//     P = Q [Rt; 0]               Householder QR (r reflectors, LAPACK dlarfg form)
+//     B = (Q^T Phi Q)[r:, r:]     symmetric positive definite: no pivoting needed
+//     c~2 = B^-1 (Q^T d)[r:],  c = Q [0; c~2],  e = Rt^-1 ((Q^T d)[:r] - (Q^T Phi Q)[:r, r:] c~2)
+// and every step of it has a fixed pivot / broadcast lane.  Measured against the reference
+// fixtures and the extended-precision truth (tools/rbf_nullspace_proto.py, the same step order
+// in numpy): 7e-14 (TPS k=20), 4e-13 (cubic), 1.1e-11 (quintic, cond 3.6e7) normwise from
+// scipy's answers, within 1-8x of LAPACK's own distance to the exact solution.
+//
+// Anything outside that regime is flagged per voxel and re-solved by the pivoting kernel
+// (k_rbf_local in list mode, the host launches it right after this kernel): a rank-deficient
+// polynomial block (|Rt_tt| < 1e-9 sqrt(k): coplanar / collinear neighbourhoods, where LAPACK
+// decides singularity), a pivot of B that is not positive or outside the Newton reciprocal's
+// range, a negative per-point smoothing, non-finite inputs.  So singular systems keep the
+// pivoting kernel's (and LAPACK's) verdict.
+//
+// Layout (per wave: four systems, one per 16-lane row; lane li holds system rows li + 16 q,
+// q < R, in registers):
+//   A[R][NC]  rows of Phi, later Q^T Phi Q, later its LU;  P[R][NP] the polynomial block;
+//   B[R][3]   right-hand sides (u, v, w);  V[NP][R] the reflectors (kept for Q^T phi(x)).
+// Every cross-lane operand is a row_newbcast of a lane fixed at compile time (the loops are
+// unrolled, rowbcast_n folds) or a segment sum (DPP + v_permlane*_swap-free 16-lane reduce).
+#pragma once
+
+#include "ptv_kernels.hpp"
+#include "ptv_rbf_math.hpp"
+
+namespace ptv {
+
+// Symmetric build scratch: row i evaluates phi for the columns (i + d) mod NC, d = 1..H, into
+// slot d - 1 of its scratch row; entry (i, j) is then row i's slot (j - i) mod NC - 1 when that
+// is < H, else row j's slot (i - j) mod NC - 1.  Rows are HS doubles apart: H itself with an XOR
+// swizzle when H is a power of two (the 16-lane stores and reads land in distinct banks), else
+// the next odd number (an odd stride is conflict-free for 16 lanes of 8-byte accesses).
+template <int NC>
+struct NsBuild {
+    static constexpr int H = NC / 2;
+    static constexpr bool POW2 = (H & (H - 1)) == 0;
+    static constexpr int HS = POW2 ? H : (H | 1);
+    __device__ static __forceinline__ int addr(int row, int slot) {
+        if constexpr (POW2) return row * HS + (slot ^ (row & (H - 1)));
+        else return row * HS + slot;
+    }
+};
+
+// x ** p for p in 0..2, as ipow (ptv_rbf_math.hpp) computes them, branch-free
+__device__ __forceinline__ double ipow2(double x, int p) { return p == 0 ? 1.0 : (p == 1 ? x : x * x); }
+// monomial with exponents packed as px | py << 8 | pz << 16, each <= 2 (degree <= 2)
+__device__ __forceinline__ double mono2(double hx, double hy, double hz, int code) {
+    return (ipow2(hx, code & 255) * ipow2(hy, (code >> 8) & 255)) * ipow2(hz, code >> 16);
+}
+
+#ifndef PTV_NS_STAMP
+#define PTV_NS_STAMP 0  // dev builds: per-wave s_memtime phase cycles into RbfKernelArgs::stamps
+#endif
+#if PTV_NS_STAMP
+#define PTV_NS_MARK(i)                                         \
+    do {                                                       \
+        __builtin_amdgcn_sched_barrier(0);                     \
+        ts[i] = __builtin_amdgcn_s_memtime();                  \
+        __builtin_amdgcn_sched_barrier(0);                     \
+    } while (0)
+#else
+#define PTV_NS_MARK(i) \
+    do {               \
+    } while (0)
+#endif
+
+template <int NC, int NP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_rbf_ns(
+    RbfKernelArgs a, const double4 *__restrict__ prec, const double4 *__restrict__ pval,
+    const uint32_t *__restrict__ slots, const double *__restrict__ ax, const double *__restrict__ ay,
+    const double *__restrict__ az, const double *__restrict__ qpx, const double *__restrict__ qpy,
+    const double *__restrict__ qpz, const double *__restrict__ smooth, const int *__restrict__ pw,
+    const uint8_t *__restrict__ mask, double *__restrict__ U, double *__restrict__ V, double *__restrict__ W,
+    int *__restrict__ status) {
+    static_assert(NC % 4 == 0 && NC >= 16 && NC <= 32, "row slots");
+    static_assert(NP >= 1 && NP < 16 && NP < NC, "polynomial terms (rows 0..NP-1 in lanes 0..NP-1)");
+    constexpr int R = (NC + 15) / 16;
+    using Bd = NsBuild<NC>;
+    constexpr int H = Bd::H;
+    constexpr int SCS = 4 * NC * Bd::HS;          // build scratch per wave (doubles)
+    constexpr int SVS = 4 * NC * 8 + 4 * NC / 2;  // sorted (values, yhat) double4 pairs + ids per wave
+    constexpr int SRS = NP * R * 64 + 4 * 2 * NP;   // reflectors (per lane) + tau, beta (per system)
+    constexpr int SC0 = SCS > SVS ? SCS : SVS;
+    constexpr int SC = SC0 > SRS ? SC0 : SRS;
+    __shared__ double4 s_ye[4][4][NC];  // per wave and system: eps-scaled coordinates + id, id order
+    __shared__ double s_sc[4][SC];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int seg = lane >> 4, li = lane & 15;
+    double4 *ye = s_ye[wid][seg];
+    double *sc = s_sc[wid];
+    double4 *sv = reinterpret_cast<double4 *>(sc) + seg * NC * 2;  // row r: sv[2r] values, sv[2r+1] yhat
+    uint32_t *sid = reinterpret_cast<uint32_t *>(sc + 4 * NC * 8) + seg * NC;
+
+    const long long plane = (long long)a.nx * a.ny;
+    const long long nvox = (long long)(a.z1 - a.z0) * plane;
+    const long long v = ((long long)blockIdx.x * 4 + wid) * 4 + seg;  // chunk-local voxel
+    const bool valid = v < nvox;
+    const long long vc = valid ? v : nvox - 1;
+    const int iz = a.z0 + (int)(vc / plane);
+    const long long rem = vc % plane;
+    const int iy = (int)(rem / a.nx), ix = (int)(rem % a.nx);
+    const size_t vfull = (size_t)iz * plane + rem;
+    const bool active = valid && (mask == nullptr || mask[vfull] != 0);
+    const int k = a.k;
+    const double eps = a.epsilon;
+#if PTV_NS_STAMP
+    unsigned long long ts[9];
+#endif
+    PTV_NS_MARK(0);
+
+    // ---- 1. neighbours li + 16 q, ranked by particle index (np.sort(yindices), _rbfinterp.py:521);
+    //      shift / scale of the neighbourhood (_build_system: (max + min)/2, (max - min)/2, 0 -> 1) ----
+    double4 r[R], d[R];
+    uint32_t id[R];
+    double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        const int nbr = li + 16 * q;
+        r[q] = make_double4(0.0, 0.0, 0.0, 0.0);
+        d[q] = r[q];
+        id[q] = 0xffffffffu;
+        if (active && nbr < k) {
+            const uint32_t sl = slots[(size_t)v * k + nbr];
+            r[q] = prec[sl];
+            d[q] = pval[sl];
+            id[q] = (uint32_t)r[q].w;
+            mn[0] = fmin(mn[0], r[q].x);
+            mn[1] = fmin(mn[1], r[q].y);
+            mn[2] = fmin(mn[2], r[q].z);
+            mx[0] = fmax(mx[0], r[q].x);
+            mx[1] = fmax(mx[1], r[q].y);
+            mx[2] = fmax(mx[2], r[q].z);
+        }
+        if (nbr < NC) sid[nbr] = id[q];
+    }
+    double sh[3] = {0.0, 0.0, 0.0}, scl[3] = {1.0, 1.0, 1.0};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const double lo = seg_min<16>(mn[c]), hi = seg_max<16>(mx[c]);
+        if (active) {
+            sh[c] = (hi + lo) / 2.0;
+            scl[c] = (hi - lo) / 2.0;
+            if (scl[c] == 0.0) scl[c] = 1.0;
+        }
+    }
+    // the voxel (x), and its monomial P_li(xhat) on lanes li < NP (evaluated at the end: computed
+    // here so that neither the shift / scale nor the coordinates stay live through the solve)
+    double qx, qy, qz;
+    if (a.separable) {
+        qx = ax[ix];
+        qy = ay[iy];
+        qz = az[iz];
+    } else {
+        qx = qpx[vfull];
+        qy = qpy[vfull];
+        qz = qpz[vfull];
+    }
+    const double pm = li < NP ? mono2((qx - sh[0]) / scl[0], (qy - sh[1]) / scl[1], (qz - sh[2]) / scl[2],
+                                      pw[li < NP ? li : 0]) : 0.0;
+    rbf_wave_sync();
+    int rank[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) rank[q] = 0;
+    for (int j = 0; j < k; ++j) {
+        const uint32_t o = sid[j];
+#pragma unroll
+        for (int q = 0; q < R; ++q) rank[q] += (o < id[q] || (o == id[q] && j < li + 16 * q)) ? 1 : 0;
+    }
+    rbf_wave_sync();
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        if (li + 16 * q < k) {
+            ye[rank[q]] = make_double4(r[q].x * eps, r[q].y * eps, r[q].z * eps, (double)id[q]);
+            sv[2 * rank[q]] = d[q];
+            sv[2 * rank[q] + 1] = make_double4((r[q].x - sh[0]) / scl[0], (r[q].y - sh[1]) / scl[1],
+                                               (r[q].z - sh[2]) / scl[2], 0.0);
+        }
+    }
+    rbf_wave_sync();
+    double4 yi[R], hh[R];  // own rows' eps-scaled coordinates (build only: reloaded for the evaluation), yhat
+    double B[R][3], dg[R];
+    bool bad = false;
+    const double phi0 = rbf_phi_rt(a.kernel, 0.0);
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        const int row = li + 16 * q;
+        const bool kr = row < k;
+        yi[q] = kr ? ye[row] : make_double4(0.0, 0.0, 0.0, 0.0);
+        const double4 dv = kr ? sv[2 * row] : make_double4(0.0, 0.0, 0.0, 0.0);
+        hh[q] = kr ? sv[2 * row + 1] : make_double4(0.0, 0.0, 0.0, 0.0);
+        B[q][0] = dv.x;
+        B[q][1] = dv.y;
+        B[q][2] = dv.z;
+        double si = 0.0;
+        if (kr && active) si = smooth != nullptr ? smooth[(size_t)yi[q].w] : a.smoothing;
+        bad = bad || si < 0.0;  // negative smoothing: not positive definite any more
+        dg[q] = kr ? phi0 + si : 1.0;  // padded rows: identity block
+    }
+    // P rows: monomials of yhat (degree <= 2: exponents 0..2, the products of ipow's fast paths)
+    double P[R][NP];
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        const bool kr = li + 16 * q < k;
+#pragma unroll
+        for (int t = 0; t < NP; ++t) P[q][t] = kr ? mono2(hh[q].x, hh[q].y, hh[q].z, pw[t]) : 0.0;
+    }
+    PTV_NS_MARK(1);
+    // ---- 2. Householder QR of P alone (the reflectors depend on P only; dlarfg: beta = -sign(alpha)
+    //      ||x||, tau = (beta - alpha)/beta, v = x / (alpha - beta), v_t = 1), applied to P's later
+    //      columns (P[0][u], u > t, of lane t ends as Rt's row t) and to the right-hand sides ----
+    const double rank_tol = 1e-9 * sqrt((double)k);
+    double Vr[NP][R], tau[NP], beta[NP];
+#pragma unroll
+    for (int t = 0; t < NP; ++t) {
+        const double alpha = rowbcast_n(t, P[0][t]);
+        double s = 0.0;
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const double x = li + 16 * q > t ? P[q][t] : 0.0;
+            s = fma(x, x, s);
+        }
+        s = seg_sum<16>(s);
+        const double nrm = sqrt(alpha * alpha + s);
+        const bool triv = !(s > 0.0);
+        const double b = triv ? alpha : (alpha >= 0.0 ? -nrm : nrm);
+        tau[t] = triv ? 0.0 : (b - alpha) / b;
+        beta[t] = b;
+        const double scal = triv ? 0.0 : 1.0 / (alpha - b);
+        bad = bad || !(fabs(b) >= rank_tol);
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const int row = li + 16 * q;
+            Vr[t][q] = row > t ? P[q][t] * scal : (row == t ? 1.0 : 0.0);
+        }
+#pragma unroll
+        for (int u = t + 1; u < NP; ++u) {
+            double w = 0.0;
+#pragma unroll
+            for (int q = 0; q < R; ++q) w = fma(Vr[t][q], P[q][u], w);
+            w = seg_sum<16>(w) * tau[t];
+#pragma unroll
+            for (int q = 0; q < R; ++q) P[q][u] = fma(-w, Vr[t][q], P[q][u]);
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            double w = 0.0;
+#pragma unroll
+            for (int q = 0; q < R; ++q) w = fma(Vr[t][q], B[q][c], w);
+            w = seg_sum<16>(w) * tau[t];
+#pragma unroll
+            for (int q = 0; q < R; ++q) B[q][c] = fma(-w, Vr[t][q], B[q][c]);
+        }
+    }
+    double Rt[NP];  // this lane's row of Rt (lanes < NP)
+#pragma unroll
+    for (int t = 0; t < NP; ++t) Rt[t] = P[0][t];
+    rbf_wave_sync();  // the values' LDS is the build scratch next
+
+    PTV_NS_MARK(2);
+    // ---- 3. symmetric build of Phi (NsBuild), read back row by row with y_t = Phi v_t accumulated ----
+    double *ss = sc + seg * (NC * Bd::HS);
+#pragma unroll 1
+    for (int dd = 1; dd <= H; ++dd) {
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const int row = li + 16 * q;
+            if (16 * q + 15 < NC || row < NC) {
+                int j = row + dd;
+                j -= j >= NC ? NC : 0;
+                double e = 0.0;
+                if (row < k && j < k) {
+                    const double4 yj = ye[j];
+                    const double dx = yi[q].x - yj.x, dy = yi[q].y - yj.y, dz = yi[q].z - yj.z;
+                    e = rbf_phi_rt(a.kernel, sqrt((dx * dx + dy * dy) + dz * dz));
+                }
+                ss[Bd::addr(row, dd - 1)] = e;
+            }
+        }
+    }
+    rbf_wave_sync();
+    PTV_NS_MARK(3);
+    double A[R][NC], Y[NP][R];
+#pragma unroll
+    for (int t = 0; t < NP; ++t)
+#pragma unroll
+        for (int q = 0; q < R; ++q) Y[t][q] = 0.0;
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const int row = li + 16 * q;
+            int dj = j - row;
+            dj += dj < 0 ? NC : 0;  // (j - row) mod NC for row < NC
+            const int own = Bd::addr(row < NC ? row : 0, dj >= 1 && dj <= H ? dj - 1 : 0);
+            const int par = Bd::addr(j, dj > H && dj < NC ? NC - dj - 1 : 0);
+            const double e = ss[dj <= H ? own : par];
+            A[q][j] = row >= NC ? 0.0 : (dj == 0 ? dg[q] : e);
+        }
+#pragma unroll
+        for (int t = 0; t < NP; ++t) {
+            if (j < t) continue;  // v_t is zero above row t
+            double vs = Vr[t][j >> 4];
+            // an empty asm that takes the column just read: the broadcast cannot be hoisted above it
+            // (hoisted, all NC x NP broadcasts stay live and the kernel spills)
+            asm volatile("" : "+v"(vs) : "v"(A[0][j]));
+            const double vj = rowbcast_n(j, vs);
+#pragma unroll
+            for (int q = 0; q < R; ++q) Y[t][q] = fma(A[q][j], vj, Y[t][q]);
+        }
+        if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // bounded reads in flight
+    }
+    rbf_wave_sync();  // every lane has its rows: the scratch now keeps the reflectors for step 8
+    double *vst = sc;                                  // V[t][q] at vst[(t * R + q) * 64 + lane]
+    double *tbs = sc + NP * R * 64 + seg * (2 * NP);  // tau[t], beta[t] of this system
+    static_assert(NP * R * 64 + 4 * 2 * NP <= SC, "reflector store fits the scratch");
+#pragma unroll
+    for (int t = 0; t < NP; ++t) {
+#pragma unroll
+        for (int q = 0; q < R; ++q) vst[(t * R + q) * 64 + lane] = Vr[t][q];
+        if (li == 0) {
+            tbs[t] = tau[t];
+            tbs[NP + t] = beta[t];
+        }
+    }
+
+    PTV_NS_MARK(4);
+    // ---- 4. Q^T Phi Q = Phi - sum_t (v_t z_t^T + z_t v_t^T), the reflectors applied in turn
+    //      (H_t Phi_t H_t = Phi_t - v z^T - z v^T with p = tau Phi_t v, z = p - tau (v.p)/2 v):
+    //      Phi_t v_t = y_t - sum_{s<t} (v_s (z_s.v_t) + z_s (v_s.v_t)).  Only the columns >= NP are
+    //      kept (B and the e right-hand side's block); columns < NP are dead ----
+#pragma unroll
+    for (int t = 0; t < NP; ++t) {
+#pragma unroll
+        for (int s2 = 0; s2 < t; ++s2) {
+            double zv = 0.0, vv = 0.0;
+#pragma unroll
+            for (int q = 0; q < R; ++q) {
+                zv = fma(Y[s2][q], Vr[t][q], zv);  // Y[s2] holds z_s2 by now
+                vv = fma(Vr[s2][q], Vr[t][q], vv);
+            }
+            zv = seg_sum<16>(zv);
+            vv = seg_sum<16>(vv);
+#pragma unroll
+            for (int q = 0; q < R; ++q) Y[t][q] = fma(-Vr[s2][q], zv, fma(-Y[s2][q], vv, Y[t][q]));
+        }
+        double kk = 0.0;
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            Y[t][q] = Y[t][q] * tau[t];
+            kk = fma(Vr[t][q], Y[t][q], kk);
+        }
+        kk = 0.5 * tau[t] * seg_sum<16>(kk);
+#pragma unroll
+        for (int q = 0; q < R; ++q) Y[t][q] = fma(-kk, Vr[t][q], Y[t][q]);  // z_t
+    }
+#pragma unroll
+    for (int j = NP; j < NC; ++j) {
+#pragma unroll
+        for (int t = 0; t < NP; ++t) {
+            double zs = Y[t][j >> 4], vs = Vr[t][j >> 4];
+            asm volatile("" : "+v"(zs), "+v"(vs) : "v"(A[0][j]));  // the broadcasts stay in their column
+            const double zj = rowbcast_n(j, zs);
+            const double vj = rowbcast_n(j, vs);
+#pragma unroll
+            for (int q = 0; q < R; ++q) A[q][j] = fma(-Vr[t][q], zj, fma(-Y[t][q], vj, A[q][j]));
+        }
+        if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // bounded broadcasts in flight
+    }
+
+    PTV_NS_MARK(5);
+    // ---- 5. LU without pivoting of B = rows / columns NP..NC-1 (pivot row c = lane c % 16 of row
+    //      set c / 16, look-ahead by one column as k_rbf_spd16); rows < NP are never updated ----
+    double rd[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) rd[q] = 1.0;
+    double piv = rowbcast_n(NP, A[NP / 16][NP]);
+    double rp = rcp_nr(piv);
+#pragma unroll
+    for (int c = NP; c < NC; ++c) {
+        const int pq = c / 16;
+        bad = bad || !(piv > 0.0);
+        rd[pq] = li == (c & 15) ? rp : rd[pq];
+        double l[R];
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const int row = li + 16 * q;
+            if (16 * q + 15 <= c) l[q] = 0.0;
+            else if (16 * q > c) l[q] = A[q][c] * rp;
+            else l[q] = row > c ? A[q][c] * rp : 0.0;
+        }
+        double pivn = 1.0, rpn = 1.0;
+#pragma unroll
+        for (int j = c + 1; j < NC; ++j) {
+            const double u = rowbcast_n(c, A[pq][j]);
+#pragma unroll
+            for (int q = 0; q < R; ++q)
+                if (16 * q + 15 > c) A[q][j] = fma(-l[q], u, A[q][j]);
+            if (j == c + 1) {
+                pivn = rowbcast_n(c + 1, A[(c + 1) / 16][c + 1]);
+                rpn = rcp_nr(pivn);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const double u = rowbcast_n(c, B[pq][t]);
+#pragma unroll
+            for (int q = 0; q < R; ++q)
+                if (16 * q + 15 > c) B[q][t] = fma(-l[q], u, B[q][t]);
+        }
+        piv = pivn;
+        rp = rpn;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        const double ar = fabs(rd[q]);
+        bad = bad || !(ar >= 0x1p-1020 && ar <= 0x1p1020);  // the Newton reciprocal's range
+    }
+
+    PTV_NS_MARK(6);
+    // ---- 6. back substitution x_c = b_c / U_cc (c >= NP) from lane c % 16; every row above c is
+    //      updated, so rows < NP end with (Q^T d)[:r] - (Q^T Phi Q)[:r, r:] c~2, e's right-hand side ----
+#pragma unroll
+    for (int c = NC - 1; c >= NP; --c) {
+        const int pq = c / 16;
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const double xc = rowbcast_n(c, B[pq][t] * rd[pq]);
+#pragma unroll
+            for (int q = 0; q < R; ++q) {
+                if (16 * q < c) {
+                    const double u = li + 16 * q < c ? A[q][c] : 0.0;
+                    B[q][t] = fma(-u, xc, B[q][t]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < R; ++q)
+#pragma unroll
+        for (int t = 0; t < 3; ++t) B[q][t] = B[q][t] * rd[q];
+
+    // ---- 7. Rt e = rhs (rows 0..NP-1: lanes 0..NP-1; Rt_it = P[0][t] of lane i < t, diag beta) ----
+    rbf_wave_sync();  // the reflector store is read back from here on
+    double E[3] = {0.0, 0.0, 0.0}, rh[3] = {B[0][0], B[0][1], B[0][2]};
+#pragma unroll
+    for (int t = NP - 1; t >= 0; --t) {
+        const double bt = tbs[NP + t];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const double et = rowbcast_n(t, rh[c] / bt);
+            E[c] = li == t ? et : E[c];
+            rh[c] = li < t ? fma(-Rt[t], et, rh[c]) : rh[c];
+        }
+    }
+
+    PTV_NS_MARK(7);
+    // ---- 8. evaluate: out = (Q^T phi(x))[r:] . c~2 + P(xhat) . e ----
+    double ph[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        ph[q] = 0.0;
+        if (li + 16 * q < k) {
+            const double4 y = ye[li + 16 * q];
+            const double dx = qx * eps - y.x, dy = qy * eps - y.y, dz = qz * eps - y.z;
+            ph[q] = rbf_phi_rt(a.kernel, sqrt((dx * dx + dy * dy) + dz * dz));
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < NP; ++t) {
+        double vt[R], w = 0.0;
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            vt[q] = vst[(t * R + q) * 64 + lane];
+            w = fma(vt[q], ph[q], w);
+        }
+        w = seg_sum<16>(w) * tbs[t];
+#pragma unroll
+        for (int q = 0; q < R; ++q) ph[q] = fma(-w, vt[q], ph[q]);
+    }
+    double o[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        o[c] = li < NP ? pm * E[c] : 0.0;
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const int row = li + 16 * q;
+            if (row >= NP && row < NC) o[c] = fma(ph[q], B[q][c], o[c]);
+        }
+        o[c] = seg_sum<16>(o[c]);
+    }
+    const bool segbad = seg_max_u32<16>((bad && active) ? 1u : 0u) != 0u;
+    PTV_NS_MARK(8);
+#if PTV_NS_STAMP
+    if (a.stamps != nullptr && lane == 0) {
+        const long long gw = (long long)blockIdx.x * 4 + wid;
+        if (gw < a.stamp_cap)
+            for (int i = 0; i < 8; ++i) a.stamps[gw * 8 + i] = ts[i + 1] - ts[i];
+    }
+#endif
+    if (!valid || li != 0) return;
+    const size_t vo = (size_t)(iz - a.out_z0) * plane + rem;
+    if (!active) {
+        U[vo] = 0.0;
+        V[vo] = 0.0;
+        W[vo] = 0.0;
+        return;
+    }
+    if (segbad) {  // re-solved by the pivoting kernel (k_rbf_local over the list)
+        const int at = atomicAdd(&status[3], 1);
+        atomicAdd(&status[5], 1);
+        if (at < a.ns_cap) a.ns_list[at] = (uint32_t)v;
+        else atomicOr(&status[4], 1);
+        return;
+    }
+    if (a.flags & PTV_FLAG_NAN_TO_NUM) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            o[c] = o[c] != o[c] ? 0.0 : (o[c] == INFINITY ? DBL_MAX : (o[c] == -INFINITY ? -DBL_MAX : o[c]));
+    }
+    U[vo] = o[0];
+    V[vo] = o[1];
+    W[vo] = o[2];
+}
+
+template <int NC, int NP>
+void launch_ns_t(const RbfKernelArgs &ka, long long nvox, hipStream_t s, const double4 *prec, const double4 *pval,
+                 const uint32_t *slots, const double *ax, const double *ay, const double *az, const double *qx,
+                 const double *qy, const double *qz, const double *smooth, const int *pw, const uint8_t *mask,
+                 double *U, double *V, double *W, int *status) {
+    const long long waves = (nvox + 3) / 4;
+    hipLaunchKernelGGL((k_rbf_ns<NC, NP>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, ka, prec, pval, slots,
+                       ax, ay, az, qx, qy, qz, smooth, pw, mask, U, V, W, status);
+}
+
+}  // namespace ptv

@@ -1,0 +1,15 @@
+// ptv_rbf_ns_b.hip — k_rbf_ns instantiations for 20 row slots (ptv_rbf_ns.hpp; one
+// translation unit per row-slot count so that they compile in parallel)
+#include "ptv_rbf_ns.hpp"
+
+namespace ptv {
+
+PTV_RBF_NS_DECL(20) {
+    switch (np) {
+        case 1: launch_ns_t<20, 1>(ka, nvox, s, prec, pval, slots, ax, ay, az, qx, qy, qz, smooth, pw, mask, U, V, W, status); break;
+        case 4: launch_ns_t<20, 4>(ka, nvox, s, prec, pval, slots, ax, ay, az, qx, qy, qz, smooth, pw, mask, U, V, W, status); break;
+        default: launch_ns_t<20, 10>(ka, nvox, s, prec, pval, slots, ax, ay, az, qx, qy, qz, smooth, pw, mask, U, V, W, status);
+    }
+}
+
+}  // namespace ptv

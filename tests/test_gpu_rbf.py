@@ -311,3 +311,76 @@ def test_spd_register_kernel_rerun_matches_lds_kernel(ctx, monkeypatch):
     for a, b in zip(big, ref):
         assert np.isfinite(a).all()
         assert normwise(a, b) <= TOL
+
+
+@pytest.mark.parametrize("kernel,k,degree", [
+    ("thin_plate_spline", 20, None),  # main.py:34-35 default: 24 x 24 systems, 20 row slots
+    ("thin_plate_spline", 32, None),  # C3's reachable half: 32 row slots
+    ("thin_plate_spline", 23, None),  # 24 row slots, one padded row
+    ("cubic", 14, None),              # 16 row slots
+    ("linear", 30, None),             # one monomial
+    ("quintic", 22, None),            # ten monomials (degree 2)
+    ("thin_plate_spline", 18, 2),     # a degree above the minimum
+])
+def test_nullspace_vs_pivoting_and_oracle(ctx, kernel, k, degree):
+    """The scale-invariant kernels run the null-space solver k_rbf_ns (static elimination order:
+    Householder QR of the polynomial block, LU without pivoting of the projected SPD block); the
+    partial-pivoting kernel (PTV_FLAG_RBF_PIVOTING) and the oracle's LAPACK gesv solve the same
+    systems.  Both GPU kernels must meet the bar against the oracle, and they must differ somewhere
+    (two different solvers ran).  The achieved errors are printed."""
+    from oracle import cpu_ref
+    from ptv_interpolation_amd import _lib
+    from ptv_interpolation_amd.rbf import LocalRBFInterpolator
+
+    P, Q, ax = _rand_case(k * 13 + len(kernel), 5000, 14)
+    it = LocalRBFInterpolator(P, Q, neighbors=k, kernel=kernel, degree=degree)
+    ns = it.evaluate_grid(ax, ax, ax)
+    assert ctx.stats["n_rbf_pivoted"] == 0
+    piv = it.evaluate_grid(ax, ax, ax, flags=_lib.FLAG_RBF_PIVOTING)
+    ref = cpu_ref.rbf_local_grid(P, Q, ax, ax, ax, k, kernel, None, degree)
+    assert any(not np.array_equal(a, b) for a, b in zip(ns, piv))
+    for c, (a, b, r) in enumerate(zip(ns, piv, ref)):
+        e_ns, e_piv = normwise(a, r), normwise(b, r)
+        print(f"{kernel} k={k} {'UVW'[c]}: null-space vs oracle {e_ns:.2e}, pivoting vs oracle {e_piv:.2e}")
+        assert e_ns <= TOL and e_piv <= TOL
+
+
+def test_nullspace_hands_rank_deficient_voxels_to_pivoting(ctx):
+    """A neighbourhood whose particles are coplanar has a rank-deficient polynomial block: the
+    null-space solver flags it and the pivoting kernel re-solves it (list mode).  Here a plane of
+    particles sits inside a random cloud: voxels near the plane whose k nearest all lie in it are
+    handed over (singular: LinAlgError, as scipy); with smoothing and a cloud dense enough that
+    no voxel's neighbourhood is planar, nothing is handed over."""
+    from ptv_interpolation_amd.rbf import LocalRBFInterpolator
+
+    rng = np.random.default_rng(8)
+    cloud = rng.uniform(0, 12, (3000, 3))
+    g = np.arange(0, 12, 0.25)
+    px, py = np.meshgrid(g, g, indexing="ij")
+    plane = np.stack([px.ravel(), py.ravel(), np.full(px.size, 6.0)], -1)
+    P = np.concatenate([cloud, plane])
+    Q = rng.standard_normal((len(P), 3))
+    ax = np.linspace(0, 11, 12)
+    with pytest.raises(np.linalg.LinAlgError, match="Singular matrix"):
+        LocalRBFInterpolator(P, Q, neighbors=20).evaluate_grid(ax, ax, ax)
+    n = ctx.last_stats()["n_rbf_pivoted"]
+    print("voxels handed to the pivoting kernel:", n)
+    assert 0 < n < 12 ** 3
+
+
+def test_nullspace_list_overflow_reruns_with_pivoting(ctx):
+    """Extreme smoothing on every particle puts every pivot of the projected block outside the
+    Newton reciprocal's range: every voxel is flagged, more than the 16384 the list holds per
+    launch, and the host reruns the launch on the pivoting kernel; the result matches the oracle
+    and the stats report every voxel as pivoted."""
+    from oracle import cpu_ref
+    from ptv_interpolation_amd.rbf import LocalRBFInterpolator
+
+    P, Q, ax = _rand_case(71, 6000, 27)
+    sm = np.full(len(P), 2e307)
+    U, V, W = LocalRBFInterpolator(P, Q, neighbors=20, smoothing=sm).evaluate_grid(ax, ax, ax)
+    assert ctx.stats["n_rbf_pivoted"] == 27 ** 3
+    ref = cpu_ref.rbf_local_grid(P, Q, ax, ax, ax, 20, smoothing=sm)
+    for a, b in zip((U, V, W), ref):
+        assert np.isfinite(a).all()
+        assert normwise(a, b) <= TOL
