@@ -255,12 +255,24 @@ def traffic_from_profiles():
     library (same SHA-256) or an earlier build."""
     import re
 
+    def round_key(f):  # traffic_r03b.json -> (3, "b"): the round order, not the checkout's mtimes
+        m = re.fullmatch(r"traffic_r(\d+)([a-z]?)\.json", os.path.basename(f))
+        return (int(m.group(1)), m.group(2))
+
     files = sorted((f for f in glob.glob(os.path.join(ROOT, "profiles", "traffic_r*.json"))
                     if re.fullmatch(r"traffic_r\d+[a-z]?\.json", os.path.basename(f))),  # not traffic_rows_*
-                   key=os.path.getmtime)
+                   key=round_key)
     if not files:
         return None, None
     try:
+        me = lib_sha256()
+        shas = {}
+        for f in files:
+            with open(f) as fh:
+                shas[f] = json.load(fh).get("lib_sha256")
+        # the profile of this very library if there is one, else the latest round's
+        pick = next((f for f in reversed(files) if shas[f] is not None and shas[f] == me), files[-1])
+        files = [pick]
         with open(files[-1]) as f:
             t = json.load(f)
         sha = t.get("lib_sha256")

@@ -67,6 +67,9 @@ extern "C" {
 /* local RBF, diagnostics: the scale-invariant kernels through the partial-pivoting solver
  * (k_rbf_local) instead of the null-space solver k_rbf_ns (ABI v9) */
 #define PTV_FLAG_RBF_PIVOTING 8u
+/* k-NN, diagnostics (k >= 13): near-tie repair list of one entry, so that a launch with two or more
+ * tiles to repair takes the whole-launch exact rerun (the path past the 2^22-tile list) (ABI v9) */
+#define PTV_FLAG_KNN_REPAIR_ALL 16u
 
 typedef struct ptv_ctx ptv_ctx;
 

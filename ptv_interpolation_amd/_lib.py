@@ -85,6 +85,7 @@ F32 = 1
 FLAG_OUT_F32 = 2  # U, V, W written as float32 (main.py:230 astype, fused)
 FLAG_RBF_SPD_LDS = 4  # local RBF diagnostics: SPD systems through the LDS-broadcast kernel
 FLAG_RBF_PIVOTING = 8  # local RBF diagnostics: scale-invariant kernels through the pivoting solver
+FLAG_KNN_REPAIR_ALL = 16  # k-NN diagnostics: near-tie repair reruns the whole launch past one tile
 
 
 class DivParams(C.Structure):

@@ -14,6 +14,8 @@
 #include <cstring>
 #include <string>
 #include <thread>
+
+#include <sys/mman.h>
 #include <vector>
 
 #include "../../include/ptv_api.h"
@@ -613,7 +615,10 @@ int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchP
         // packed-key lists: the near-tie repair list (tiles whose order the keys did not prove;
         // a handful per launch: past the cap the whole launch reruns exact)
         const long long tiles = (long long)((g->nx + 3) / 4) * ((g->ny + 3) / 4) * ((z1 - z0 + 3) / 4);
-        const int cap = (int)std::max<long long>(1, std::min<long long>(tiles, 1LL << 22));
+        // (PTV_FLAG_KNN_REPAIR_ALL: a one-entry list, so any second listed tile reruns the whole launch)
+        const int cap = (prm->flags & PTV_FLAG_KNN_REPAIR_ALL)
+                            ? 1
+                            : (int)std::max<long long>(1, std::min<long long>(tiles, 1LL << 22));
         PTV_TRY(c->rep_cnt.ensure(1));
         PTV_TRY(c->rep_list.ensure((size_t)cap));
         kl.rep_cnt = c->rep_cnt.p;
@@ -1005,6 +1010,8 @@ struct EventSet {
 // faults are taken in parallel here (a write per page; the D2H then overwrites every byte), so
 // only the copy remains on the critical path.  Joined before the D2H is enqueued, and on every
 // early return.
+constexpr int kMadvPopulateWrite = 23;  // MADV_POPULATE_WRITE (Linux 5.14), absent from older headers
+
 struct PageToucher {
     std::vector<std::thread> th;
     void start(void *const *bufs, int nbuf, size_t bytes) {
@@ -1018,11 +1025,18 @@ struct PageToucher {
             std::vector<char *> b(nbuf);
             for (int i = 0; i < nbuf; ++i) b[i] = static_cast<char *>(bufs[i]);
             th.emplace_back([b, p0, p1, bytes]() {
-                for (char *base : b)
+                // fault the pages in writable WITHOUT changing them (a failed call must leave the
+                // caller's arrays as they were): MADV_POPULATE_WRITE where the kernel has it, else a
+                // volatile read-modify-write of one byte per page
+                for (char *base : b) {
+                    const uintptr_t lo = (reinterpret_cast<uintptr_t>(base) + p0 * kPage) & ~(uintptr_t)(kPage - 1);
+                    const uintptr_t hi = reinterpret_cast<uintptr_t>(base) + std::min(p1 * kPage, bytes);
+                    if (hi > lo && madvise(reinterpret_cast<void *>(lo), hi - lo, kMadvPopulateWrite) == 0) continue;
                     for (size_t pg = p0; pg < p1; ++pg) {
                         volatile char *q = base + std::min(pg * kPage, bytes - 1);
-                        *q = 0;
+                        *q = *q;
                     }
+                }
             });
         }
     }

@@ -21,15 +21,30 @@ _ROOT = os.path.dirname(os.path.abspath(__file__))
 _SHADOWED = ("interpolator", "filtering", "physics")
 
 
+# files that mark a directory as the reference's layout (its entry scripts)
+_MARKERS = ("main.py", "run_porous_glass.py", "interpolate_porous_glass.py", "test_parallel.py", "analyze_flow.py")
+_NOTED = set()
+
+
 def _reference_shadows(name):
-    """The first other ``name.py`` on sys.path sits next to a ``main.py`` (the reference layout).
-    Any other module of that name is left alone; with none, the normal import finds the shim."""
+    """The first other ``name.py`` on sys.path sits next to one of the reference's entry scripts
+    (the reference layout).  Any other module of that name is left alone, with a one-time note on
+    stderr (it then runs on the CPU; ``PTV_DROPIN=0`` silences it); with none, the normal import
+    finds the shim."""
     for d in sys.path:
         d = os.path.abspath(d or os.getcwd())
         if d == _ROOT:
             continue
-        if os.path.isfile(os.path.join(d, name + ".py")):
-            return os.path.isfile(os.path.join(d, "main.py"))
+        f = os.path.join(d, name + ".py")
+        if os.path.isfile(f):
+            if any(os.path.isfile(os.path.join(d, m)) for m in _MARKERS):
+                return True
+            if name not in _NOTED:
+                _NOTED.add(name)
+                print(f"ptv_interpolation_amd drop-in: {f} is not next to a reference entry script "
+                      f"({', '.join(_MARKERS)}); importing it unchanged (CPU). PTV_DROPIN=0 silences this.",
+                      file=sys.stderr)
+            return False
     return False
 
 

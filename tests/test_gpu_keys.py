@@ -87,6 +87,28 @@ def test_lattice_ties_repair(ctx, k):
             assert np.array_equal(a, b), f"{np.sum(a != b)} voxels differ"
 
 
+def test_lattice_ties_whole_launch_rerun(ctx):
+    """The repair list past its capacity (PTV_FLAG_KNN_REPAIR_ALL: a one-entry list) reruns the
+    whole launch with the exact pair lists: the result is bit-identical to the listed-tile rerun and
+    to the oracle, with more tiles to repair than the list holds."""
+    from oracle import cpu_ref
+    from ptv_interpolation_amd import _lib
+
+    g = np.arange(0.0, 14.0)
+    Z, Y, X = np.meshgrid(g, g, g, indexing="ij")
+    P = np.stack([X.ravel(), Y.ravel(), Z.ravel()], -1)
+    Q = np.tile([1.5, -2.0, 0.25], (len(P), 1))
+    ax = np.arange(0.5, 13.0, 1.0)
+    listed = ctx.interp_knn(P, Q, axes=(ax, ax, ax), k=20)
+    whole = ctx.interp_knn(P, Q, axes=(ax, ax, ax), k=20, flags=_lib.FLAG_KNN_REPAIR_ALL)
+    rep = ctx.stats["n_repair_tiles"]
+    print(f"whole-launch rerun: tiles to repair {rep}")
+    assert rep > 1
+    ref = cpu_ref.interp_grid(P, Q, ax, ax, ax, "idw", 20, 2.0)
+    for a, b, c in zip(listed, whole, ref):
+        assert np.array_equal(a, b) and np.array_equal(b, c)
+
+
 @pytest.mark.parametrize("k", [16, 40])
 def test_lattice_plus_random_ties(ctx, k):
     """A spacing-4 particle lattice mixed with random particles (random values): exact ties
