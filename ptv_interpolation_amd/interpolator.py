@@ -261,11 +261,27 @@ def _knn_field(points, values, grid_tuple, method, k, power, radius=0.0):
          "idw_radius": _lib.METHOD_IDW_RADIUS}[method]
     axes = separable_axes(X, Y, Z)
     if axes is not None:
-        # z-slab per device (launcher.py); bit-identical to one whole-grid call
-        full = [np.empty((len(axes[2]), len(axes[1]), len(axes[0]))) for _ in range(3)]
-        U, V, W = launcher.run_slabs(len(axes[2]), lambda ctx, z0, z1, views: ctx.interp_knn(
-            points, values, axes=axes, method=m, k=k, power=power, eps=_EPS, z_range=(z0, z1), out=views,
-            radius=radius), full)
+        # z-slab per device (launcher.py); bit-identical to one whole-grid call.  With several
+        # slabs each one bins only the particles within a halo of its planes (slab_halo: the library
+        # proves the cull exact from its lattice bounds or says which halo would be; interp_slab
+        # retries with it), as the north_star z-slab partition does (zslab.py)
+        from . import zslab
+
+        nz = len(axes[2])
+        halo0 = 0.0
+        if launcher.slab_count(nz) > 1 and method != "idw_radius":
+            halo0 = zslab.halo_guess(n, [float(np.max(a) - np.min(a)) for a in axes], k)
+
+        def slab(ctx, z0, z1, views):
+            def call(h):
+                ctx.interp_knn(points, values, axes=axes, method=m, k=k, power=power, eps=_EPS, z_range=(z0, z1),
+                               out=views, radius=radius, slab_halo=h)
+                return ctx.stats
+
+            return zslab.interp_slab(call, zslab.HaloState(halo0)) if halo0 > 0.0 else call(0.0)
+
+        full = [np.empty((nz, len(axes[1]), len(axes[0]))) for _ in range(3)]
+        U, V, W = launcher.run_slabs(nz, slab, full)
     else:
         ctx = _lib.Context.get(launcher.devices()[0])
         size = int(np.prod(shape))

@@ -3,10 +3,12 @@
 
 Every voxel depends only on the particle set and its own coordinate, and a z-slab call of
 the kernels produces the same bits as the same planes of a whole-grid call, so the grid's
-z planes are split into contiguous slabs, one per device, each device bins the full
-(replicated) particle set and interpolates its slab, and the slabs land in disjoint
-slices of the caller's output.  One host thread per device drives its own context and
-stream (ctypes releases the GIL during the C calls); no collective touches the data path.
+z planes are split into contiguous slabs, one per device, each device interpolates its slab
+from the (replicated) particle set, and the slabs land in disjoint slices of the caller's
+output.  The k-NN methods bin only the particles near their slab (ptv_knn_params.slab_halo,
+proven exact from the coarse-lattice bounds, zslab.interp_slab's retry when it is not).  One
+host thread per device drives its own context and stream (ctypes releases the GIL during the C
+calls); no collective touches the data path.
 
 Devices: ``PTV_DEVICE=i`` pins one device; ``PTV_DEVICES=0,1,...`` lists them (a device
 may repeat: several contexts, one per slab, on the same GPU); default all visible GPUs.
@@ -23,6 +25,7 @@ from . import _lib
 
 _ctx_lock = threading.Lock()
 _slab_ctx = {}
+last_results = []  # what fn returned for each slab of the last run_slabs call (slab order)
 
 
 def devices():
@@ -63,9 +66,10 @@ def run_slabs(nz: int, fn, out):
     for a in out:
         if not (a.flags.c_contiguous and a.shape[0] == nz):
             raise ValueError("run_slabs: outputs must be C-contiguous with nz leading planes")
+    global last_results
     devs = devices()
     if len(devs) <= 1 or nz < 2:
-        fn(_lib.Context.get(devs[0]), 0, nz, out)
+        last_results = [fn(_lib.Context.get(devs[0]), 0, nz, out)]
         return out
     slabs = slab_bounds(nz, len(devs))
     seen = {}
@@ -75,5 +79,11 @@ def run_slabs(nz: int, fn, out):
         seen[d] = slot + 1
         jobs.append((context(d, slot), z0, z1, tuple(a[z0:z1] for a in out)))
     with ThreadPoolExecutor(len(jobs)) as ex:
-        list(ex.map(lambda j: fn(*j), jobs))
+        last_results = list(ex.map(lambda j: fn(*j), jobs))
     return out
+
+
+def slab_count(nz: int) -> int:
+    """How many slabs run_slabs cuts an nz-plane grid into."""
+    n = len(devices())
+    return 1 if n <= 1 or nz < 2 else min(n, nz)

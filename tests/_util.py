@@ -117,6 +117,28 @@ def hetero_ties(points, values, ax, ay, az, k):
     return tie.reshape(X.shape), het.reshape(X.shape)
 
 
+def tie_value_bounds(points, values, ax, ay, az, k, extra=64):
+    """Per-voxel (lo, hi), each (C, nz, ny, nx): min / max of every value component over the
+    particles any correct k-NN search may pick (the first k plus the whole run tied with the k-th
+    distance).  IDW and Sibson outputs are positive-weight averages of their neighbours' values, so
+    whatever the tie order they lie in [lo, hi] (up to rounding)."""
+    from scipy.spatial import KDTree
+
+    P = np.asarray(points, dtype=np.float64)
+    Vv = np.asarray(values, dtype=np.float64).reshape(len(P), -1)
+    Z, Y, X = np.meshgrid(az, ay, ax, indexing="ij")
+    q = np.stack([X.ravel(), Y.ravel(), Z.ravel()], -1)
+    kk = min(k + extra, len(P))
+    d, i = KDTree(P).query(q, k=kk, workers=-1)
+    d = d.reshape(len(q), -1)
+    i = i.reshape(len(q), -1)
+    cand = d <= d[:, k - 1:k]  # (Q, kk): within the k-th distance
+    vals = Vv[i]  # (Q, kk, C)
+    lo = np.where(cand[..., None], vals, np.inf).min(axis=1).T.reshape((-1,) + X.shape)
+    hi = np.where(cand[..., None], vals, -np.inf).max(axis=1).T.reshape((-1,) + X.shape)
+    return lo, hi
+
+
 def filter_ties(points, k):
     """(n,) bool: particles whose remove_outliers_knn decision depends on cKDTree's tie order.
 

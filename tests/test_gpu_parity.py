@@ -15,11 +15,14 @@ import numpy as np
 import pandas as pd
 import pytest
 
-from tests._util import hetero_ties, load, names, normwise
+from tests._util import hetero_ties, load, names, normwise, tie_value_bounds
 
 pytestmark = pytest.mark.gpu
 
 TOL = 1e-10
+# the most a fixture may lose to value-heterogeneous ties (excluded from the bit / normwise
+# comparison): the edge fixtures are built to have them (coincident particles, sigma = 0 lattices)
+EXCLUDED_MAX = {"edge_sibson_sigma0": 0.50, "edge_coincident_idw": 0.15, "edge_coincident_sibson": 0.15}
 
 
 @pytest.fixture(scope="module")
@@ -54,7 +57,17 @@ def test_golden_parity(ctx, name):
         tie, het = hetero_ties(g["points"], g["values"], g["ax"], g["ay"], g["az"], int(g["k"]))
         print(f"{name}: ties {tie.mean():.4%}, value-heterogeneous (excluded) {het.mean():.4%}")
         keep = ~het
-        assert keep.mean() > 0.5
+        assert het.mean() <= EXCLUDED_MAX.get(name, 0.02)
+        # on the excluded voxels, what no tie order changes: the NaN pattern (sigma = 0, empty
+        # weights) and a value inside the range of the candidate neighbours' values
+        lo, hi = tie_value_bounds(g["points"], g["values"], g["ax"], g["ay"], g["az"], int(g["k"]))
+        for c, (a, b) in enumerate(((U, g["U"]), (V, g["V"]), (W, g["W"]))):
+            assert np.array_equal(np.isnan(a[het]), np.isnan(b[het]))
+            fin = het & ~np.isnan(a)
+            span = np.maximum(np.abs(lo[c][fin]), np.abs(hi[c][fin])) * 1e-12
+            assert ((a[fin] >= lo[c][fin] - span) & (a[fin] <= hi[c][fin] + span)).all()
+            print(f"{name} {'UVW'[c]}: excluded voxels {het.sum()}, NaN {np.isnan(a[het]).sum()}, "
+                  f"all finite ones inside their candidates' value range")
     for a, b in ((U, g["U"]), (V, g["V"]), (W, g["W"])):
         assert normwise(a[keep], b[keep]) <= TOL
         same = np.mean((a[keep] == b[keep]) | (np.isnan(a[keep]) & np.isnan(b[keep])))
