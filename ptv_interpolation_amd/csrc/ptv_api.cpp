@@ -431,7 +431,7 @@ struct SearchParams {
 // Fills `kl` with a launch template for planes [z_begin, z_end) of the grid.
 int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchParams *prm, const double *ax,
             const double *ay, const double *az, const double *qx, const double *qy, const double *qz, hipStream_t s,
-            KnnLaunch &kl, Binned &bout) {
+            KnnLaunch &kl, Binned &bout, const double *known_bbox = nullptr) {
     const int64_t n = p->n;
     const bool sep = ax != nullptr;
     const int64_t plane = g->nx * g->ny;
@@ -458,11 +458,14 @@ int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchP
         qn[0] = qn[1] = qn[2] = nvox;
     }
     PTV_HIP(hipEventRecord(c->ev_bin0, s));
-    PTV_TRY(launch_bbox(pp, n, qa, qn, c->bbox_part.p, 1024, c->bbox_out.p, s));
-    PTV_HIP(hipMemcpyAsync(c->h_bbox, c->bbox_out.p, 6 * sizeof(double), hipMemcpyDeviceToHost, s));
-    PTV_HIP(hipStreamSynchronize(s));
-    double lo[3] = {c->h_bbox[0], c->h_bbox[1], c->h_bbox[2]};
-    double hi[3] = {c->h_bbox[3], c->h_bbox[4], c->h_bbox[5]};
+    if (known_bbox == nullptr) {  // (the slab cull reads it back together with its kept count)
+        PTV_TRY(launch_bbox(pp, n, qa, qn, c->bbox_part.p, 1024, c->bbox_out.p, s));
+        PTV_HIP(hipMemcpyAsync(c->h_bbox, c->bbox_out.p, 6 * sizeof(double), hipMemcpyDeviceToHost, s));
+        PTV_HIP(hipStreamSynchronize(s));
+        known_bbox = c->h_bbox;
+    }
+    double lo[3] = {known_bbox[0], known_bbox[1], known_bbox[2]};
+    double hi[3] = {known_bbox[3], known_bbox[4], known_bbox[5]};
     for (int a = 0; a < 3; ++a) {
         if (!std::isfinite(lo[a]) || !std::isfinite(hi[a])) {
             set_error("non-finite particle or grid coordinates");
@@ -673,7 +676,17 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
         uint32_t *h_total = reinterpret_cast<uint32_t *>(c->h_misc);
         PTV_HIP(hipEventRecord(c->ev_cull0, s));
         PTV_TRY(launch_cull(src, n, az, (int)g->z_begin, (int)g->z_end, prm->slab_halo, c->cull_win.p,
-                            c->cull_cnt.p, dst, h_total, s));
+                            c->cull_cnt.p, dst, nullptr, s));
+        // the kept particles' bounding box (with the slab's query planes) from the count on the device,
+        // read back with the count: one host synchronisation for the cull and the cell grid
+        PTV_TRY(c->bbox_part.ensure(6 * 1024));
+        PTV_TRY(c->bbox_out.ensure(8));
+        const double *kp[3] = {dst[0], dst[1], dst[2]};
+        const double *qa[3] = {ax, ay, az + g->z_begin};
+        const int64_t qn[3] = {g->nx, g->ny, g->z_end - g->z_begin};
+        PTV_TRY(launch_bbox(kp, n, qa, qn, c->bbox_part.p, 1024, c->bbox_out.p, s, c->cull_cnt.p + nb));
+        PTV_HIP(hipMemcpyAsync(c->h_bbox, c->bbox_out.p, 6 * sizeof(double), hipMemcpyDeviceToHost, s));
+        PTV_HIP(hipMemcpyAsync(h_total, c->cull_cnt.p + nb, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
         PTV_HIP(hipEventRecord(c->ev_cull1, s));
         PTV_HIP(hipStreamSynchronize(s));
         const int64_t kept = (int64_t)*h_total;
@@ -683,7 +696,7 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
             c->cull_timed = true;
         }
     }
-    PTV_TRY(prepare(c, &pe, g, &sp, ax, ay, az, qx, qy, qz, s, kl, b));
+    PTV_TRY(prepare(c, &pe, g, &sp, ax, ay, az, qx, qy, qz, s, kl, b, culled ? c->h_bbox : nullptr));
     if (culled && kl.cb.dk == nullptr) {
         // no lattice bounds were built, so nothing proves the cull exact: bin every particle
         // instead (same result as slab_halo = 0), never refuse the call for it
@@ -692,25 +705,14 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
         PTV_TRY(prepare(c, p, g, &sp, ax, ay, az, qx, qy, qz, s, kl, b));
     }
     if (culled) {
+        // the exactness proof runs on the device and gates the main launch (it writes nothing
+        // unless the halo is proven); the host reads the proof back after it, so no
+        // synchronisation stalls the stream between the lattice and the main launch
         PTV_TRY(c->halo_need.ensure(1));
         PTV_TRY(launch_halo_need(kl.cb.ax, kl.cb.ay, kl.cb.az, kl.cb.n[0], kl.cb.n[1], kl.cb.n[2], kl.cb.dk,
                                  c->cull_win.p, kl.cg.mg, c->halo_need.p, s));
-        PTV_HIP(hipMemcpyAsync(c->h_misc + 1, c->halo_need.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
-        PTV_HIP(hipStreamSynchronize(s));
-        double need;
-        std::memcpy(&need, &c->h_misc[1], sizeof(need));
-        c->last.n_particles = p->n;
-        c->last.n_binned = pe.n;
-        c->last.halo_required = need;
-        c->timed_pending = true;  // bin / lattice / cull timings of this call stay readable
-        if (!(need <= prm->slab_halo)) {
-            PTV_HIP(hipEventRecord(c->ev_main0, s));  // no main launch: empty kernel interval
-            PTV_HIP(hipEventRecord(c->ev_knn1, s));
-            if (st) *st = c->last;  // halo_required for the caller's retry
-            set_error("slab cull not proven exact: slab_halo " + std::to_string(prm->slab_halo) +
-                      " < required " + std::to_string(need) + " (retry with >= halo_required, or 0)");
-            return PTV_E_INEXACT;
-        }
+        kl.gate = c->halo_need.p;
+        kl.gate_halo = prm->slab_halo;
         PTV_HIP(hipEventRecord(c->ev_main0, s));
     }
     c->rbf_chunks = 0;
@@ -721,6 +723,21 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
     PTV_TRY(launch_knn(kl, b, ax, ay, az, qx, qy, qz, mask, U, V, W, s));
     PTV_HIP(hipEventRecord(c->ev_knn1, s));
     c->timed_pending = true;
+    if (culled) {
+        PTV_HIP(hipMemcpyAsync(c->h_misc + 1, c->halo_need.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+        PTV_HIP(hipStreamSynchronize(s));
+        double need;
+        std::memcpy(&need, &c->h_misc[1], sizeof(need));
+        c->last.n_particles = p->n;
+        c->last.n_binned = pe.n;
+        c->last.halo_required = need;
+        if (!(need <= prm->slab_halo)) {
+            if (st) *st = c->last;  // halo_required for the caller's retry
+            set_error("slab cull not proven exact: slab_halo " + std::to_string(prm->slab_halo) +
+                      " < required " + std::to_string(need) + " (retry with >= halo_required, or 0)");
+            return PTV_E_INEXACT;
+        }
+    }
     if (st) *st = c->last;
     return PTV_OK;
 }

@@ -30,6 +30,7 @@ struct BBoxArgs {
     const double *q[3];
     int64_t n;
     int64_t qn[3];
+    const uint32_t *dn;  // particle count on the device (the slab cull's), or NULL: n
 };
 
 __global__ __launch_bounds__(256) void k_bbox(BBoxArgs a, double *partials) {
@@ -41,7 +42,8 @@ __global__ __launch_bounds__(256) void k_bbox(BBoxArgs a, double *partials) {
     }
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (int64_t i = t0; i < a.n; i += stride) {
+    const int64_t np = a.dn != nullptr ? (int64_t)*a.dn : a.n;
+    for (int64_t i = t0; i < np; i += stride) {
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
             double v = a.p[d][i];
@@ -106,8 +108,9 @@ __global__ __launch_bounds__(256) void k_bbox_final(const double *partials, int 
 }
 
 int launch_bbox(const double *const px[3], int64_t n, const double *const qa[3], const int64_t qn[3],
-                double *d_partials, int max_blocks, double *d_out6, hipStream_t s) {
+                double *d_partials, int max_blocks, double *d_out6, hipStream_t s, const uint32_t *d_n) {
     BBoxArgs a;
+    a.dn = d_n;
     int64_t m = n;
     for (int d = 0; d < 3; ++d) {
         a.p[d] = px[d];
@@ -438,7 +441,7 @@ int launch_cull(const double *const src[6], int64_t n, const double *az, int z0,
     }
     hipLaunchKernelGGL(k_cull_write, dim3(nb), dim3(256), 0, s, c, n, (const double *)win, (const uint32_t *)bcount);
     PTV_HIP(hipGetLastError());
-    PTV_HIP(hipMemcpyAsync(h_total, bcount + nb, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    if (h_total != nullptr) PTV_HIP(hipMemcpyAsync(h_total, bcount + nb, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     return PTV_OK;
 }
 

@@ -9,7 +9,8 @@ namespace ptv {
 // Per-axis min/max over the particles and the query coordinates.
 // Query coordinates: separable axes (qa[a] has qn[a] entries) or point lists.
 int launch_bbox(const double *const px[3], int64_t n, const double *const qa[3], const int64_t qn[3],
-                double *d_partials, int max_blocks, double *d_out6, hipStream_t s);
+                double *d_partials, int max_blocks, double *d_out6, hipStream_t s,
+                const uint32_t *d_n = nullptr);  // d_n: the particle count on the device (<= n)
 
 // Counting-sort the particles into linear-order cells (deterministic order
 // inside each cell: ascending original index).  Scratch buffers must hold
@@ -22,7 +23,8 @@ size_t scan_partials_needed(size_t m);
 
 // slab cull (ptv_knn_params.slab_halo): win (4 doubles) = (zlo, zhi, slab z min, slab z max),
 // bcount: cull_blocks(n) + 1 scratch words; the kept count is copied to the HOST word *h_total
-// (pinned; valid after the stream synchronises).  Order-preserving.
+// (pinned; valid after the stream synchronises; NULL: left on the device in bcount[cull_blocks(n)]).
+// Order-preserving.
 size_t cull_blocks(int64_t n);
 int launch_cull(const double *const src[6], int64_t n, const double *az, int z0, int z1, double halo, double *win,
                 uint32_t *bcount, double *const dst[6], uint32_t *h_total, hipStream_t s);
@@ -83,6 +85,9 @@ struct KnnLaunch {
     int rep_cap = 0;
     unsigned int *h_rep = nullptr;
     int64_t *n_repair = nullptr;
+    // slab cull proof gate (see KnnKernelArgs::gate): NULL = always run
+    const unsigned long long *gate = nullptr;
+    double gate_halo = 0.0;
 };
 
 // Longest-first dispatch order for a lattice-level k-NN launch over (nx, ny, nz) points: each

@@ -328,6 +328,8 @@ int launch_knn(const KnnLaunch &a, const Binned &b, const double *ax, const doub
         return PTV_E_ARG;
     }
     ka.order = a.order;
+    ka.gate = a.gate;
+    ka.gate_halo = a.gate_halo;
     // union seeds (k > 8): the first ~3/4 of each corner's list; the 8 corners' union still holds
     // k distinct particles (else the lattice bound): 512^3 / 5M same-box, IDW k = 50 115.4 ->
     // 114.1 ms at 36 of 50, Sibson k = 30 58.4 -> 57.5 ms at 22 of 30

@@ -114,6 +114,10 @@ struct KnnKernelArgs {
     int rep_cap;
     const uint32_t *tiles;  // repair launch: the listed tiles (wave e of the launch takes tiles[e])
     int ntiles;
+    // slab cull: the proven halo (a double's bits, launch_halo_need) and the halo binned; the
+    // launch does nothing unless gate_halo >= proven (the host reads the proof after it)
+    const unsigned long long *gate;
+    double gate_halo;
 };
 
 // Packed keys (the KMAX >= 16 lists).  A key is the candidate's exact f64 d2 with the low B
@@ -634,6 +638,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
     constexpr bool KEYS = kKeyList<KMAX, EXACT>;
     const int lb = (int)(blockIdx.y * gridDim.x + blockIdx.x);  // linear dispatch order
     if (lb >= a.nblocks) return;                                  // 2-D grid padding (block-uniform)
+    if (a.gate != nullptr && !(__longlong_as_double((long long)*a.gate) <= a.gate_halo))
+        return;  // slab cull not proven exact: no outputs (the call returns PTV_E_INEXACT)
     int b, tw;  // block of the tile grid, wave (x-tile) within it
     if (a.tiles != nullptr) {
         // repair launch: wave e takes the e-th listed tile (wave-uniform exit)

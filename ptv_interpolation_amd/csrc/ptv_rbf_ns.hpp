@@ -81,6 +81,19 @@ __device__ __forceinline__ double mono2(double hx, double hy, double hz, int cod
     } while (0)
 #endif
 
+// phi of the scale-invariant kernels from the squared distance d2 = r^2 (scipy's
+// _rbfinterp_pythran forms up to rounding: the thin-plate spline as d2 log(d2) / 2, which needs no
+// square root; r^3 = d2 r, -r^5 = -(d2 d2) r).  A few ulps from scipy's r**2*log(r), far inside
+// what the solve amplifies (cond <= ~1e7 for these systems: 1e-9 relative at worst, 1e-13 typical).
+__device__ __forceinline__ double phi_ns(int kern, double d2) {
+    switch (kern) {
+        case PTV_RBF_THIN_PLATE_SPLINE: return d2 == 0.0 ? 0.0 : (0.5 * d2) * log(d2);
+        case PTV_RBF_CUBIC: return d2 * sqrt_spd(d2);
+        case PTV_RBF_QUINTIC: return -((d2 * d2) * sqrt_spd(d2));
+        default: return -sqrt_spd(d2);  // linear
+    }
+}
+
 template <int NC, int NP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_rbf_ns(
     RbfKernelArgs a, const double4 *__restrict__ prec, const double4 *__restrict__ pval,
@@ -197,7 +210,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     double4 yi[R], hh[R];  // own rows' eps-scaled coordinates (build only: reloaded for the evaluation), yhat
     double B[R][3], dg[R];
     bool bad = false;
-    const double phi0 = rbf_phi_rt(a.kernel, 0.0);
+    const double phi0 = phi_ns(a.kernel, 0.0);
 #pragma unroll
     for (int q = 0; q < R; ++q) {
         const int row = li + 16 * q;
@@ -288,7 +301,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
                 if (row < k && j < k) {
                     const double4 yj = ye[j];
                     const double dx = yi[q].x - yj.x, dy = yi[q].y - yj.y, dz = yi[q].z - yj.z;
-                    e = rbf_phi_rt(a.kernel, sqrt((dx * dx + dy * dy) + dz * dz));
+                    e = phi_ns(a.kernel, (dx * dx + dy * dy) + dz * dz);
                 }
                 ss[Bd::addr(row, dd - 1)] = e;
             }
@@ -316,11 +329,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 #pragma unroll
         for (int t = 0; t < NP; ++t) {
             if (j < t) continue;  // v_t is zero above row t
-            double vs = Vr[t][j >> 4];
-            // an empty asm that takes the column just read: the broadcast cannot be hoisted above it
-            // (hoisted, all NC x NP broadcasts stay live and the kernel spills)
-            asm volatile("" : "+v"(vs) : "v"(A[0][j]));
-            const double vj = rowbcast_n(j, vs);
+            const double vj = rowbcast_n(j, Vr[t][j >> 4]);
 #pragma unroll
             for (int q = 0; q < R; ++q) Y[t][q] = fma(A[q][j], vj, Y[t][q]);
         }
@@ -374,10 +383,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     for (int j = NP; j < NC; ++j) {
 #pragma unroll
         for (int t = 0; t < NP; ++t) {
-            double zs = Y[t][j >> 4], vs = Vr[t][j >> 4];
-            asm volatile("" : "+v"(zs), "+v"(vs) : "v"(A[0][j]));  // the broadcasts stay in their column
-            const double zj = rowbcast_n(j, zs);
-            const double vj = rowbcast_n(j, vs);
+            const double zj = rowbcast_n(j, Y[t][j >> 4]);
+            const double vj = rowbcast_n(j, Vr[t][j >> 4]);
 #pragma unroll
             for (int q = 0; q < R; ++q) A[q][j] = fma(-Vr[t][q], zj, fma(-Y[t][q], vj, A[q][j]));
         }
@@ -462,10 +469,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     double E[3] = {0.0, 0.0, 0.0}, rh[3] = {B[0][0], B[0][1], B[0][2]};
 #pragma unroll
     for (int t = NP - 1; t >= 0; --t) {
-        const double bt = tbs[NP + t];
+        const double rbt = 1.0 / tbs[NP + t];
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            const double et = rowbcast_n(t, rh[c] / bt);
+            const double et = rowbcast_n(t, rh[c] * rbt);
             E[c] = li == t ? et : E[c];
             rh[c] = li < t ? fma(-Rt[t], et, rh[c]) : rh[c];
         }
@@ -480,7 +487,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         if (li + 16 * q < k) {
             const double4 y = ye[li + 16 * q];
             const double dx = qx * eps - y.x, dy = qy * eps - y.y, dz = qz * eps - y.z;
-            ph[q] = rbf_phi_rt(a.kernel, sqrt((dx * dx + dy * dy) + dz * dz));
+            ph[q] = phi_ns(a.kernel, (dx * dx + dy * dy) + dz * dz);
         }
     }
 #pragma unroll
