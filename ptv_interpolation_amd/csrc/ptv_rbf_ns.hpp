@@ -65,6 +65,73 @@ __device__ __forceinline__ double mono2(double hx, double hy, double hz, int cod
     return (ipow2(hx, code & 255) * ipow2(hy, (code >> 8) & 255)) * ipow2(hz, code >> 16);
 }
 
+
+// ---- v_fmac_f64 with its first operand broadcast from lane N of the 16-lane row (gfx950 DPALU
+// DPP: row_newbcast only): acc += src[lane N] * mul in ONE instruction where the compiler emits a
+// v_mov_b64_dpp and a v_fma_f64 (it does not fold 64-bit DPP into the fmac).  Inline asm, so the
+// compiler cannot see the DPP read: each block starts with the s_nop 1 (2 wait states) a DPP read
+// needs after a VALU write of its source.  A block updates the accumulators of every live row set
+// of the lane (RS = 1 or 2) with one broadcast source. ----
+template <int N, int RS>
+__device__ __forceinline__ void fmac_bc(double (&acc)[RS], double src, const double (&mul)[RS]) {
+    if constexpr (RS == 1) {
+        asm("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+            : "+v"(acc[0]) : "v"(src), "v"(mul[0]), "n"(N));
+    } else {
+        asm("s_nop 1\n\tv_fmac_f64_dpp %0, %2, %3 row_newbcast:%5 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f64_dpp %1, %2, %4 row_newbcast:%5 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+            : "+v"(acc[0]), "+v"(acc[1]) : "v"(src), "v"(mul[0]), "v"(mul[1]), "n"(N));
+    }
+}
+// the same where the source is the accumulator `piv` itself (the pivot row's set): the other set
+// `oth` first, then piv (its DPP read precedes its write)
+template <int N>
+__device__ __forceinline__ void fmac_bc_piv(double &oth, double &piv, double m_oth, double m_piv) {
+    asm("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f64_dpp %1, %1, %3 row_newbcast:%4 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+        : "+v"(oth), "+v"(piv) : "v"(m_oth), "v"(m_piv), "n"(N));
+}
+template <int N>
+__device__ __forceinline__ void fmac_bc_self(double &piv, double m_piv) {
+    asm("s_nop 1\n\tv_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+        : "+v"(piv) : "v"(m_piv), "n"(N));
+}
+#define PTV_NS_SW16(n, CALL)      \
+    switch ((n) & 15) {           \
+        case 0: CALL(0); break;   \
+        case 1: CALL(1); break;   \
+        case 2: CALL(2); break;   \
+        case 3: CALL(3); break;   \
+        case 4: CALL(4); break;   \
+        case 5: CALL(5); break;   \
+        case 6: CALL(6); break;   \
+        case 7: CALL(7); break;   \
+        case 8: CALL(8); break;   \
+        case 9: CALL(9); break;   \
+        case 10: CALL(10); break; \
+        case 11: CALL(11); break; \
+        case 12: CALL(12); break; \
+        case 13: CALL(13); break; \
+        case 14: CALL(14); break; \
+        default: CALL(15); break; \
+    }
+template <int RS>
+__device__ __forceinline__ void fmac_bc_n(int n, double (&acc)[RS], double src, const double (&mul)[RS]) {
+#define PTV_C(N) fmac_bc<N, RS>(acc, src, mul)
+    PTV_NS_SW16(n, PTV_C)
+#undef PTV_C
+}
+__device__ __forceinline__ void fmac_bc_piv_n(int n, double &oth, double &piv, double m_oth, double m_piv) {
+#define PTV_C(N) fmac_bc_piv<N>(oth, piv, m_oth, m_piv)
+    PTV_NS_SW16(n, PTV_C)
+#undef PTV_C
+}
+__device__ __forceinline__ void fmac_bc_self_n(int n, double &piv, double m_piv) {
+#define PTV_C(N) fmac_bc_self<N>(piv, m_piv)
+    PTV_NS_SW16(n, PTV_C)
+#undef PTV_C
+}
+
 #ifndef PTV_NS_STAMP
 #define PTV_NS_STAMP 0  // dev builds: per-wave s_memtime phase cycles into RbfKernelArgs::stamps
 #endif
@@ -329,9 +396,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 #pragma unroll
         for (int t = 0; t < NP; ++t) {
             if (j < t) continue;  // v_t is zero above row t
-            const double vj = rowbcast_n(j, Vr[t][j >> 4]);
+            double col[R];
 #pragma unroll
-            for (int q = 0; q < R; ++q) Y[t][q] = fma(A[q][j], vj, Y[t][q]);
+            for (int q = 0; q < R; ++q) col[q] = A[q][j];
+            fmac_bc_n<R>(j, Y[t], Vr[t][j >> 4], col);  // Y_t += A[:, j] v_t[j]
         }
         if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // bounded reads in flight
     }
@@ -379,15 +447,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 #pragma unroll
         for (int q = 0; q < R; ++q) Y[t][q] = fma(-kk, Vr[t][q], Y[t][q]);  // z_t
     }
+    double nV[NP][R], nY[NP][R];  // negated: A += nY v[j] + nV z[j], each an fmac with the broadcast folded
+#pragma unroll
+    for (int t = 0; t < NP; ++t)
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            nV[t][q] = -Vr[t][q];
+            nY[t][q] = -Y[t][q];
+        }
 #pragma unroll
     for (int j = NP; j < NC; ++j) {
+        double col[R];
+#pragma unroll
+        for (int q = 0; q < R; ++q) col[q] = A[q][j];
 #pragma unroll
         for (int t = 0; t < NP; ++t) {
-            const double zj = rowbcast_n(j, Y[t][j >> 4]);
-            const double vj = rowbcast_n(j, Vr[t][j >> 4]);
-#pragma unroll
-            for (int q = 0; q < R; ++q) A[q][j] = fma(-Vr[t][q], zj, fma(-Y[t][q], vj, A[q][j]));
+            fmac_bc_n<R>(j, col, Vr[t][j >> 4], nY[t]);  // - z_t v_t[j]
+            fmac_bc_n<R>(j, col, Y[t][j >> 4], nV[t]);   // - v_t z_t[j]
         }
+#pragma unroll
+        for (int q = 0; q < R; ++q) A[q][j] = col[q];
         if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // bounded broadcasts in flight
     }
 
@@ -404,21 +483,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         const int pq = c / 16;
         bad = bad || !(piv > 0.0);
         rd[pq] = li == (c & 15) ? rp : rd[pq];
+        // negated multipliers (A += l u, the pivot row's u broadcast inside the fmac); the live row
+        // sets are pq..R-1 (a set wholly above the pivot is finished)
+        const double nrp = -rp;
         double l[R];
 #pragma unroll
         for (int q = 0; q < R; ++q) {
             const int row = li + 16 * q;
             if (16 * q + 15 <= c) l[q] = 0.0;
-            else if (16 * q > c) l[q] = A[q][c] * rp;
-            else l[q] = row > c ? A[q][c] * rp : 0.0;
+            else if (16 * q > c) l[q] = A[q][c] * nrp;
+            else l[q] = row > c ? A[q][c] * nrp : 0.0;
         }
         double pivn = 1.0, rpn = 1.0;
 #pragma unroll
         for (int j = c + 1; j < NC; ++j) {
-            const double u = rowbcast_n(c, A[pq][j]);
-#pragma unroll
-            for (int q = 0; q < R; ++q)
-                if (16 * q + 15 > c) A[q][j] = fma(-l[q], u, A[q][j]);
+            if (R == 2 && pq == 0) fmac_bc_piv_n(c, A[R - 1][j], A[0][j], l[R - 1], l[0]);
+            else fmac_bc_self_n(c, A[pq][j], l[pq]);
             if (j == c + 1) {
                 pivn = rowbcast_n(c + 1, A[(c + 1) / 16][c + 1]);
                 rpn = rcp_nr(pivn);
@@ -426,10 +506,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         }
 #pragma unroll
         for (int t = 0; t < 3; ++t) {
-            const double u = rowbcast_n(c, B[pq][t]);
-#pragma unroll
-            for (int q = 0; q < R; ++q)
-                if (16 * q + 15 > c) B[q][t] = fma(-l[q], u, B[q][t]);
+            if (R == 2 && pq == 0) fmac_bc_piv_n(c, B[R - 1][t], B[0][t], l[R - 1], l[0]);
+            else fmac_bc_self_n(c, B[pq][t], l[pq]);
         }
         piv = pivn;
         rp = rpn;
@@ -447,15 +525,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 #pragma unroll
     for (int c = NC - 1; c >= NP; --c) {
         const int pq = c / 16;
+        double u[R];  // this lane's U entries of column c (rows above c), the rest 0
+#pragma unroll
+        for (int q = 0; q < R; ++q) u[q] = li + 16 * q < c ? A[q][c] : 0.0;
 #pragma unroll
         for (int t = 0; t < 3; ++t) {
-            const double xc = rowbcast_n(c, B[pq][t] * rd[pq]);
-#pragma unroll
-            for (int q = 0; q < R; ++q) {
-                if (16 * q < c) {
-                    const double u = li + 16 * q < c ? A[q][c] : 0.0;
-                    B[q][t] = fma(-u, xc, B[q][t]);
-                }
+            const double nx = -(B[pq][t] * rd[pq]);  // -x_c on lane c % 16
+            if (R == 2 && pq == 1) {
+                double bb[2] = {B[0][t], B[R - 1][t]};
+                const double uu[2] = {u[0], u[R - 1]};
+                fmac_bc_n<2>(c, bb, nx, uu);
+                B[0][t] = bb[0];
+                B[R - 1][t] = bb[1];
+            } else {
+                double bb[1] = {B[0][t]};
+                const double uu[1] = {u[0]};
+                fmac_bc_n<1>(c, bb, nx, uu);
+                B[0][t] = bb[0];
             }
         }
     }
