@@ -174,7 +174,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     constexpr int R = (NC + 15) / 16;
     using Bd = NsBuild<NC>;
     constexpr int H = Bd::H;
-    constexpr int SCS = 4 * NC * Bd::HS;          // build scratch per wave (doubles)
+    // build scratch per wave (doubles): up to 20 row slots the full symmetric matrix (row stride
+    // NC + 1, odd: conflict-free 16-lane rows and columns; every entry read back with a constant
+    // offset, no per-entry address arithmetic), above that the half-matrix scheme of NsBuild
+    constexpr bool FULL = NC <= 20;
+    constexpr int MS = NC + 1;
+    constexpr int SCS = FULL ? 4 * NC * MS : 4 * NC * Bd::HS;
     constexpr int SVS = 4 * NC * 8 + 4 * NC / 2;  // sorted (values, yhat) double4 pairs + ids per wave
     constexpr int SRS = NP * R * 64 + 4 * 2 * NP;   // reflectors (per lane) + tau, beta (per system)
     constexpr int SC0 = SCS > SVS ? SCS : SVS;
@@ -355,7 +360,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 
     PTV_NS_MARK(2);
     // ---- 3. symmetric build of Phi (NsBuild), read back row by row with y_t = Phi v_t accumulated ----
-    double *ss = sc + seg * (NC * Bd::HS);
+    double *ss = sc + seg * (FULL ? NC * MS : NC * Bd::HS);
+    if constexpr (FULL) {
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const int row = li + 16 * q;
+            if (16 * q + 15 < NC || row < NC) ss[row * MS + row] = dg[q];
+        }
+    }
 #pragma unroll 1
     for (int dd = 1; dd <= H; ++dd) {
 #pragma unroll
@@ -370,7 +382,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
                     const double dx = yi[q].x - yj.x, dy = yi[q].y - yj.y, dz = yi[q].z - yj.z;
                     e = phi_ns(a.kernel, (dx * dx + dy * dy) + dz * dz);
                 }
-                ss[Bd::addr(row, dd - 1)] = e;
+                if constexpr (FULL) {
+                    ss[row * MS + j] = e;
+                    ss[j * MS + row] = e;
+                } else {
+                    ss[Bd::addr(row, dd - 1)] = e;
+                }
             }
         }
     }
@@ -386,12 +403,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 #pragma unroll
         for (int q = 0; q < R; ++q) {
             const int row = li + 16 * q;
-            int dj = j - row;
-            dj += dj < 0 ? NC : 0;  // (j - row) mod NC for row < NC
-            const int own = Bd::addr(row < NC ? row : 0, dj >= 1 && dj <= H ? dj - 1 : 0);
-            const int par = Bd::addr(j, dj > H && dj < NC ? NC - dj - 1 : 0);
-            const double e = ss[dj <= H ? own : par];
-            A[q][j] = row >= NC ? 0.0 : (dj == 0 ? dg[q] : e);
+            if constexpr (FULL) {
+                // lanes past the last row slot read a real row (finite values; those rows never
+                // pivot and never reach an output)
+                const int rr = row < NC ? row : row - 16;
+                A[q][j] = ss[rr * MS + j];
+            } else {
+                int dj = j - row;
+                dj += dj < 0 ? NC : 0;  // (j - row) mod NC for row < NC
+                const int own = Bd::addr(row < NC ? row : 0, dj >= 1 && dj <= H ? dj - 1 : 0);
+                const int par = Bd::addr(j, dj > H && dj < NC ? NC - dj - 1 : 0);
+                const double e = ss[dj <= H ? own : par];
+                A[q][j] = row >= NC ? 0.0 : (dj == 0 ? dg[q] : e);
+            }
         }
 #pragma unroll
         for (int t = 0; t < NP; ++t) {

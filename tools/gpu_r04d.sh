@@ -1,7 +1,18 @@
+#!/bin/bash
+# Round 4 mid-round GPU check: RBF / launcher / parity tests, null-space kernel stamps, TPS lines,
+# the --share rehearsal.  usage: gpurun -- bash tools/gpu_r04d.sh [tag]
 set -o pipefail
-mkdir -p gpurun_out/r04d
-timeout -k 10 600 python -u -m pytest tests/test_gpu_launcher.py tests/test_gpu_parity.py "tests/test_gpu_keys.py::test_lattice_ties_whole_launch_rerun" -x -v -s --timeout 300 --timeout-method thread > gpurun_out/r04d/tests.log 2>&1 || { echo TESTS FAILED; tail -40 gpurun_out/r04d/tests.log; exit 1; }
-tail -3 gpurun_out/r04d/tests.log
-grep -E "binned per slab|excluded voxels|whole-launch" gpurun_out/r04d/tests.log | head -20
-PTV_LIB=ab/libptv_nsst.so timeout -k 10 300 python -u tools/ns_stamps.py 256 625000 20 32 > gpurun_out/r04d/stamps.txt 2>&1; cat gpurun_out/r04d/stamps.txt
-bash tools/gpu_r04_share.sh r04d_share
+tag=${1:-r04d}
+cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
+out=gpurun_out/$tag
+mkdir -p "$out"
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests/test_gpu_rbf.py tests/test_gpu_launcher.py tests/test_gpu_parity.py "tests/test_gpu_keys.py::test_lattice_ties_whole_launch_rerun" -x -v -s --timeout 300 --timeout-method thread > "$out/tests.log" 2>&1 || { echo TESTS FAILED; tail -40 "$out/tests.log"; exit 1; }
+tail -2 "$out/tests.log"
+grep -E "binned per slab|whole-launch|null-space vs oracle" "$out/tests.log" | head -30
+PTV_LIB=ab/libptv_nsst.so timeout -k 10 300 python -u tools/ns_stamps.py 256 625000 20 32 > "$out/stamps.txt" 2>&1; cat "$out/stamps.txt"
+for kk in 20 32; do
+  timeout -k 10 300 python -u bench.py --method rbf --k $kk --steps 3 --warmup 1 --no-cpu-baseline > "$out/tps$kk.json" 2> "$out/tps$kk.err" || { echo "BENCH FAILED k=$kk"; tail -20 "$out/tps$kk.err"; exit 1; }
+  python -c "import json,sys; l=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1], l['roofline'])" "$out/tps$kk.json"
+done
+bash tools/gpu_r04_share.sh ${tag}_share
