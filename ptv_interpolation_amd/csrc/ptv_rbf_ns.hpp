@@ -148,13 +148,39 @@ __device__ __forceinline__ void fmac_bc_self_n(int n, double &piv, double m_piv)
     } while (0)
 #endif
 
+// log(x) for finite x > 0 within ~2 ulp (fdlibm's e_log reduction and minimax polynomial: x =
+// 2^e m, m in [sqrt(1/2), sqrt(2)), f = m - 1, s = f / (2 + f), log(m) = f - (f^2/2 - s (f^2/2 +
+// R(s^2)))), with s from v_rcp_f64 + one Newton step: ~30 VALU where the device libm's
+// double-double log takes ~85.  The thin-plate spline's entries only need a few ulps.
+__device__ __forceinline__ double log_ns(double x) {
+    double m = __builtin_amdgcn_frexp_mant(x);
+    int e = __builtin_amdgcn_frexp_exp(x);
+    const bool lo = m < 0x1.6a09e667f3bcdp-1;  // sqrt(1/2)
+    m = lo ? m + m : m;
+    e = lo ? e - 1 : e;
+    const double f = m - 1.0;
+    const double d = 2.0 + f;
+    double r = __builtin_amdgcn_rcp(d);
+    r = fma(r, fma(-d, r, 1.0), r);
+    const double sv = f * r;
+    const double z = sv * sv, w = z * z;
+    const double t1 = w * fma(w, fma(w, 1.531383769920937332e-01, 2.222219843214978396e-01), 3.999999999940941908e-01);
+    const double t2 =
+        z * fma(w, fma(w, fma(w, 1.479819860511658591e-01, 1.818357216161805012e-01), 2.857142874366239149e-01),
+                6.666666666666735130e-01);
+    const double R = t2 + t1;
+    const double hfsq = 0.5 * f * f;
+    const double de = (double)e;
+    return de * 6.93147180369123816490e-01 - ((hfsq - fma(sv, hfsq + R, de * 1.90821492927058770002e-10)) - f);
+}
+
 // phi of the scale-invariant kernels from the squared distance d2 = r^2 (scipy's
 // _rbfinterp_pythran forms up to rounding: the thin-plate spline as d2 log(d2) / 2, which needs no
 // square root; r^3 = d2 r, -r^5 = -(d2 d2) r).  A few ulps from scipy's r**2*log(r), far inside
 // what the solve amplifies (cond <= ~1e7 for these systems: 1e-9 relative at worst, 1e-13 typical).
 __device__ __forceinline__ double phi_ns(int kern, double d2) {
     switch (kern) {
-        case PTV_RBF_THIN_PLATE_SPLINE: return d2 == 0.0 ? 0.0 : (0.5 * d2) * log(d2);
+        case PTV_RBF_THIN_PLATE_SPLINE: return d2 == 0.0 ? 0.0 : (0.5 * d2) * log_ns(d2);
         case PTV_RBF_CUBIC: return d2 * sqrt_spd(d2);
         case PTV_RBF_QUINTIC: return -((d2 * d2) * sqrt_spd(d2));
         default: return -sqrt_spd(d2);  // linear
@@ -368,26 +394,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
             if (16 * q + 15 < NC || row < NC) ss[row * MS + row] = dg[q];
         }
     }
+    // the NC x H (row i, column (i + d) mod NC) entries as one list dealt round-robin over the 16
+    // lanes (ceil(NC H / 16) phi per lane: 13 at 20 slots, 18 at 24, where one row per lane-set
+    // costs R H = 20, 24), each written where the read-back finds it
+    constexpr int NSLOT = NC * H;
+    constexpr int SPL = (NSLOT + 15) / 16;
 #pragma unroll 1
-    for (int dd = 1; dd <= H; ++dd) {
-#pragma unroll
-        for (int q = 0; q < R; ++q) {
-            const int row = li + 16 * q;
-            if (16 * q + 15 < NC || row < NC) {
-                int j = row + dd;
-                j -= j >= NC ? NC : 0;
-                double e = 0.0;
-                if (row < k && j < k) {
-                    const double4 yj = ye[j];
-                    const double dx = yi[q].x - yj.x, dy = yi[q].y - yj.y, dz = yi[q].z - yj.z;
-                    e = phi_ns(a.kernel, (dx * dx + dy * dy) + dz * dz);
-                }
-                if constexpr (FULL) {
-                    ss[row * MS + j] = e;
-                    ss[j * MS + row] = e;
-                } else {
-                    ss[Bd::addr(row, dd - 1)] = e;
-                }
+    for (int sl = 0; sl < SPL; ++sl) {
+        const int p = sl * 16 + li;
+        if (NSLOT % 16 == 0 || p < NSLOT) {
+            const int dd = p / NC + 1, i = p - (dd - 1) * NC;
+            int j = i + dd;
+            j -= j >= NC ? NC : 0;
+            double e = 0.0;
+            if (i < k && j < k) {
+                const double4 yv = ye[i], yj = ye[j];
+                const double dx = yv.x - yj.x, dy = yv.y - yj.y, dz = yv.z - yj.z;
+                e = phi_ns(a.kernel, (dx * dx + dy * dy) + dz * dz);
+            }
+            if constexpr (FULL) {
+                ss[i * MS + j] = e;
+                ss[j * MS + i] = e;
+            } else {
+                ss[Bd::addr(i, dd - 1)] = e;
             }
         }
     }
