@@ -67,6 +67,16 @@ namespace ptv {
 #define PTV_KNN_KEYI_2W 40  // key-list interpolation kernels of at least this many slots: 2 waves per SIMD
 #endif
 
+#ifndef PTV_KNN_UNROLL_MAX
+// key-list interpolation epilogues up to this many slots unroll their blocks at compile time;
+// longer lists run the rolled passes
+#define PTV_KNN_UNROLL_MAX 32
+#endif
+#ifndef PTV_KNN_KEEP_MAX
+// key lists up to this many slots keep the epilogue's distances (then weights) in registers
+// between passes; longer ones re-gather the records every pass
+#define PTV_KNN_KEEP_MAX 32
+#endif
 #ifndef PTV_STAMP_SEEDSPLIT
 #define PTV_STAMP_SEEDSPLIT 0  // dev stamp builds: union-seed counting passes stamped as 'setup'
 #endif
@@ -626,6 +636,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
     __shared__ int lds_owner[4][64];
     // kModeRadius: the value records of the buffered candidates (the weights are summed in the flush)
     __shared__ double4 lds_val[4][MODE == kModeRadius ? kCap : 1];
+    // key-list interpolation (k >= 13): the final slot lists in LDS, lane-major ([entry][lane] u32),
+    // in this wave's candidate buffer (free once the search is done) and, past its kCap * 8 words,
+    // lds_kx: the epilogue's passes read their blocks of 8 slots from here instead of holding KMAX
+    // slot registers (and rotating them per block)
+    constexpr bool KSLI = kKeyList<KMAX, EXACT> && MODE == kModeInterp;
+    constexpr int KSLN = KSLI ? KMAX * 64 : 0;
+    constexpr int KCW = kCap * 8;
+    __shared__ uint32_t lds_kx[4][KSLN > KCW ? KSLN - KCW : 1];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     double4 *buf = lds_cand[wid];
@@ -1532,25 +1550,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
     // key lists: the k + 1 entries' slots, shifted to 0..k (kpad uniform), and the (k+1)-th
     // key's near-tie with the k-th (before the shift: compile-time slots)
     constexpr bool KSL = KEYS && MODE != kModeKDist;
-    int ksl[KSL ? KMAX : 1];
+    constexpr bool KSLR = KSL && !KSLI;  // slot list in registers (filter, slots modes)
+    int ksl[KSLR ? KMAX : 1];
+    auto ksl_word = [&](int j) -> uint32_t * {
+        return j * 64 < KCW ? reinterpret_cast<uint32_t *>(lds_cand[wid]) + j * 64 + lane : &lds_kx[wid][j * 64 - KCW + lane];
+    };
     bool amb = false;
     if constexpr (KSL) {
         amb = active && bd[KMAX - 1] < INFINITY && same_trunc(bd[KMAX - 2], bd[KMAX - 1], a.smask);
+        if constexpr (KSLI) {
+            wave_lds_sync();  // every lane is done with the candidate buffer
 #pragma unroll
-        for (int j = 0; j < KMAX; ++j) ksl[j] = (int)key_slot(bd[j], a.smask);
-        if constexpr (MODE != kModeSlots) {
+            for (int j = 0; j < KMAX; ++j) {
+                const int pos = j - a.kpad;  // shifted so that the k + 1 entries are 0 .. k
+                if (pos >= 0) *ksl_word(pos) = key_slot(bd[j], a.smask);
+            }
+            wave_lds_sync();
+        } else {
 #pragma unroll
-            for (int sh = 1; sh < KMAX; sh <<= 1) {
-                if (a.kpad & sh) {
+            for (int j = 0; j < KMAX; ++j) ksl[j] = (int)key_slot(bd[j], a.smask);
+            if constexpr (MODE != kModeSlots) {
 #pragma unroll
-                    for (int j = 0; j + sh < KMAX; ++j) ksl[j] = ksl[j + sh];
+                for (int sh = 1; sh < KMAX; sh <<= 1) {
+                    if (a.kpad & sh) {
+#pragma unroll
+                        for (int j = 0; j + sh < KMAX; ++j) ksl[j] = ksl[j + sh];
+                    }
                 }
             }
         }
     }
     // slot of list entry j (after the shift)
     auto slot_at = [&](int j) -> int {
-        if constexpr (KSL) return ksl[j];
+        if constexpr (KSLI) return (int)*ksl_word(j);
+        else if constexpr (KSL) return ksl[j];
         else return bp[j];
     };
     // exact d2 of the first n listed entries in ascending order (key lists), in blocks of 8
@@ -1657,7 +1690,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
         store_out(a.flags, U, V, W, vo, o[0], o[1], o[2]);
         return;
     }
-    if constexpr (KSL && MODE == kModeInterp && KMAX <= 32) {
+    if constexpr (KSL && MODE == kModeInterp && KMAX <= PTV_KNN_UNROLL_MAX) {
         // up to 32 slots: blocks unrolled at compile time (the loads of different blocks overlap,
         // measured faster than the rolled loop below at 3 waves per SIMD: Sibson k = 30 79 vs 92 ms)
         // Key lists (k >= 13): the weights are streamed in blocks of 8 neighbours from the exact
@@ -1665,7 +1698,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
         // interpolator.py:142-153 (IDW), :102-122 (Sibson).  Register-kept distances where the
         // list is short enough, record re-gathers otherwise.
         const int k = a.k;
-        constexpr bool KEEP = KMAX <= 32;
+        constexpr bool KEEP = KMAX <= PTV_KNN_KEEP_MAX;
         double dk[KEEP ? KMAX : 1];  // Sibson: d_j, IDW: d2_j
         auto d2_block = [&](int m, double (&d2)[8]) {
             double4 rc[8];
@@ -1674,9 +1707,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
 #pragma unroll
             for (int i = 0; i < 8; ++i) d2[i] = exact_d2(rc[i]);
         };
-        auto val_block = [&](int m, double4 (&vv)[8]) {
+        // u, v, w of 8 value records straight into the product arrays (24 of the 32 bytes: 48
+        // registers in flight, not 64 plus the products)
+        auto val_block = [&](int m, double (&tu)[8], double (&tv)[8], double (&tw)[8]) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) vv[i] = pval[m + i < k ? slot_at(min(m + i, KMAX - 1)) : slot_at(0)];
+            for (int i = 0; i < 8; ++i) {
+                const double *r = reinterpret_cast<const double *>(
+                    pval + (m + i < k ? slot_at(min(m + i, KMAX - 1)) : slot_at(0)));
+                const double2 uv = *reinterpret_cast<const double2 *>(r);
+                tu[i] = uv.x;
+                tv[i] = uv.y;
+                tw[i] = r[2];
+            }
         };
         double out[3];
         bool ok = true;
@@ -1785,9 +1827,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
 #pragma unroll
             for (int m = 0; m < KMAX; m += 8) {
                 if (m < k) {
-                    double4 vv[8];
-                    val_block(m, vv);
                     double w[8], tu[8], tv[8], tw8[8];
+                    val_block(m, tu, tv, tw8);
                     if constexpr (KEEP) {
 #pragma unroll
                         for (int i = 0; i < 8; ++i) w[i] = dk[min(m + i, KMAX - 1)];
@@ -1797,9 +1838,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
 #pragma unroll
                     for (int i = 0; i < 8; ++i) {
                         const double wn = fast ? div_by(w[i], s2, rs2) : w[i] / s2;
-                        tu[i] = wn * vv[i].x;
-                        tv[i] = wn * vv[i].y;
-                        tw8[i] = wn * vv[i].z;
+                        tu[i] = wn * tu[i];
+                        tv[i] = wn * tv[i];
+                        tw8[i] = wn * tw8[i];
                     }
                     pu.add(m, k, tu);
                     pv.add(m, k, tv);
@@ -1846,9 +1887,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
 #pragma unroll
             for (int m = 0; m < KMAX; m += 8) {
                 if (m < k) {
-                    double4 vv[8];
-                    val_block(m, vv);
                     double d2[8], tu[8], tv[8], tw8[8];
+                    val_block(m, tu, tv, tw8);
                     if constexpr (KEEP) {
 #pragma unroll
                         for (int i = 0; i < 8; ++i) d2[i] = dk[min(m + i, KMAX - 1)];
@@ -1859,9 +1899,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                     for (int i = 0; i < 8; ++i) {
                         const double w = 1.0 / (np_pow(sqrt_cr(d2[i]), a.power) + a.eps);
                         const double wn = fast ? div_by(w, s, rs) : w / s;
-                        tu[i] = wn * vv[i].x;
-                        tv[i] = wn * vv[i].y;
-                        tw8[i] = wn * vv[i].z;
+                        tu[i] = wn * tu[i];
+                        tv[i] = wn * tv[i];
+                        tw8[i] = wn * tw8[i];
                     }
                     pu.add(m, k, tu);
                     pv.add(m, k, tv);
@@ -1886,28 +1926,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
         // blocks (a fully unrolled epilogue was tens of KB of straight-line code per wave): block
         // b takes slots 0..7 of a copy of the slot list that is rotated down by 8 per block.
         const int k = a.k;
-        // ksl rotates circularly by 8 per block; rewind() completes the turn after a pass
-        int rot = 0;  // blocks rotated so far (mod KMAX / 8)
-        auto rotate8 = [&]() {
-            int t[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) t[i] = ksl[i];
-#pragma unroll
-            for (int j = 0; j + 8 < KMAX; ++j) ksl[j] = ksl[j + 8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) ksl[KMAX - 8 + i] = t[i];
-        };
-        auto rewind = [&]() {
-#pragma unroll 1
-            for (; rot != 0 && rot < KMAX / 8; ++rot) rotate8();
-            rot = 0;
-        };
+        // the slots of block m from the LDS slot list (entries past k: entry 0's, a valid slot)
+        auto rewind = [&]() {};
         auto next_slots = [&](int m, int (&s8)[8]) {
-            const int s0 = ksl[0];
+            const int s0 = slot_at(0);
 #pragma unroll
-            for (int i = 0; i < 8; ++i) s8[i] = m + i < k ? ksl[i] : s0;
-            rotate8();
-            ++rot;
+            for (int i = 0; i < 8; ++i) s8[i] = m + i < k ? slot_at(m + i) : s0;
         };
         // x, y, z of 8 records (24 of each 32-byte record: 48 VGPRs in flight, not 64)
         auto xyz_block = [&](const double4 *__restrict__ src, const int (&s8)[8], double (&x)[8], double (&y)[8],
