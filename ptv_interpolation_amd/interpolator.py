@@ -278,7 +278,13 @@ def _knn_field(points, values, grid_tuple, method, k, power, radius=0.0):
                                out=views, radius=radius, slab_halo=h)
                 return ctx.stats
 
-            return zslab.interp_slab(call, zslab.HaloState(halo0)) if halo0 > 0.0 else call(0.0)
+            if halo0 <= 0.0:
+                return call(0.0)
+            hs = zslab.HaloState(halo0)
+            st = dict(zslab.interp_slab(call, hs))
+            st["halo_state"] = hs.as_dict()  # the halo tried first / last, and the retries
+            st["halo_first"] = halo0
+            return st
 
         full = [np.empty((nz, len(axes[1]), len(axes[0]))) for _ in range(3)]
         U, V, W = launcher.run_slabs(nz, slab, full)

@@ -72,10 +72,12 @@ class HaloState:
         return {"halo": self.halo, "required": self.required, "retries": self.retries}
 
 
-def interp_slab(call, state: HaloState, max_tries: int = 3):
+def interp_slab(call, state: HaloState, max_tries: int = 4):
     """``call(halo) -> stats dict`` (a ``Context.interp_knn_dev`` bound to this rank's slab);
-    on ``InexactError`` retry with the halo the library proved sufficient, last resort 0 (every
-    particle binned, nothing to prove)."""
+    on ``InexactError`` retry with the halo the library proved sufficient, at least 1.25x the one
+    refused (the proof of a wider cull is computed on a different particle set and lattice, so its
+    requirement can come out higher again: in sphere-pack voids the requirement grew over two or
+    three retries by 1x steps), last resort 0 (every particle binned, nothing to prove)."""
     for _ in range(max_tries):
         try:
             st = call(state.halo)
@@ -84,7 +86,8 @@ def interp_slab(call, state: HaloState, max_tries: int = 3):
         except _lib.InexactError as e:
             state.retries += 1
             h = e.halo_required
-            state.halo = h * (1.0 + 1e-6) if (h is not None and math.isfinite(h) and h > 0) else 0.0
+            state.halo = (max(h * (1.0 + 1e-6), 1.25 * state.halo)
+                          if (h is not None and math.isfinite(h) and h > 0) else 0.0)
             if state.halo == 0.0:
                 break
     state.halo = 0.0

@@ -7,7 +7,7 @@ cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 out=gpurun_out/$tag
 mkdir -p "$out"
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests/test_gpu_rbf.py tests/test_gpu_keys.py tests/test_gpu_launcher.py tests/test_gpu_parity.py -x -v -s --timeout 300 --timeout-method thread > "$out/tests.log" 2>&1 || { echo TESTS FAILED; tail -40 "$out/tests.log"; exit 1; }
+timeout -k 10 900 python -u -m pytest tests/test_gpu_launcher.py tests/test_gpu_parity.py -v -s --timeout 300 --timeout-method thread > "$out/tests.log" 2>&1 || { echo TESTS FAILED; tail -40 "$out/tests.log"; exit 1; }
 tail -2 "$out/tests.log"
 grep -E "binned per slab|whole-launch|null-space vs oracle" "$out/tests.log" | head -30
 PTV_LIB=ab/libptv_nsst.so timeout -k 10 300 python -u tools/ns_stamps.py 256 625000 20 32 > "$out/stamps.txt" 2>&1; cat "$out/stamps.txt"
