@@ -39,6 +39,7 @@
 
 #include "ptv_kernels.hpp"
 #include "ptv_rbf_math.hpp"
+#include "ptv_log_table.hpp"
 
 namespace ptv {
 
@@ -57,6 +58,26 @@ struct NsBuild {
         else return row * HS + slot;
     }
 };
+
+// _monomial_powers(3, degree) (_rbfinterp.py:48-79; monomial_powers in ptv_api.cpp) packed px | py
+// << 8 | pz << 16: degree 0 is the first entry, degree 1 the first 4, degree 2 all 10 (the order is
+// by degree, so NP alone fixes every exponent)
+constexpr int kNsPow[10] = {0, 1, 256, 65536, 2, 1 | 256, 1 | 65536, 512, 256 | 65536, 131072};
+template <int C>
+__device__ __forceinline__ double ipow_c(double x) {
+    if constexpr (C == 0) return 1.0;
+    else if constexpr (C == 1) return x;
+    else return x * x;
+}
+template <int T, int NP>
+__device__ __forceinline__ void ns_prow(double (&row)[NP], const double4 &h, bool kr) {
+    if constexpr (T < NP) {
+        constexpr int c = kNsPow[T];
+        if constexpr (T == 0) row[T] = kr ? 1.0 : 0.0;
+        else row[T] = (ipow_c<(c & 255)>(h.x) * ipow_c<((c >> 8) & 255)>(h.y)) * ipow_c<(c >> 16)>(h.z);
+        ns_prow<T + 1, NP>(row, h, kr);
+    }
+}
 
 // x ** p for p in 0..2, as ipow (ptv_rbf_math.hpp) computes them, branch-free
 __device__ __forceinline__ double ipow2(double x, int p) { return p == 0 ? 1.0 : (p == 1 ? x : x * x); }
@@ -148,44 +169,104 @@ __device__ __forceinline__ void fmac_bc_self_n(int n, double &piv, double m_piv)
     } while (0)
 #endif
 
-// log(x) for finite x > 0 within ~2 ulp (fdlibm's e_log reduction and minimax polynomial: x =
-// 2^e m, m in [sqrt(1/2), sqrt(2)), f = m - 1, s = f / (2 + f), log(m) = f - (f^2/2 - s (f^2/2 +
-// R(s^2)))), with s from v_rcp_f64 + one Newton step: ~30 VALU where the device libm's
-// double-double log takes ~85.  The thin-plate spline's entries only need a few ulps.
-__device__ __forceinline__ double log_ns(double x) {
-    double m = __builtin_amdgcn_frexp_mant(x);
-    int e = __builtin_amdgcn_frexp_exp(x);
-    const bool lo = m < 0x1.6a09e667f3bcdp-1;  // sqrt(1/2)
-    m = lo ? m + m : m;
-    e = lo ? e - 1 : e;
-    const double f = m - 1.0;
-    const double d = 2.0 + f;
-    double r = __builtin_amdgcn_rcp(d);
-    r = fma(r, fma(-d, r, 1.0), r);
-    const double sv = f * r;
-    const double z = sv * sv, w = z * z;
-    const double t1 = w * fma(w, fma(w, 1.531383769920937332e-01, 2.222219843214978396e-01), 3.999999999940941908e-01);
-    const double t2 =
-        z * fma(w, fma(w, fma(w, 1.479819860511658591e-01, 1.818357216161805012e-01), 2.857142874366239149e-01),
-                6.666666666666735130e-01);
-    const double R = t2 + t1;
-    const double hfsq = 0.5 * f * f;
-    const double de = (double)e;
-    return de * 6.93147180369123816490e-01 - ((hfsq - fma(sv, hfsq + R, de * 1.90821492927058770002e-10)) - f);
+// log(x) for finite x > 0 within ~3 ulp by table reduction (tools/gen_log_table.py): x = m 2^e,
+// the bin of m's top 9 fraction bits gives y = f m in [3/4, 3/2) with exponent e' and (s = f/c, T =
+// log c); r = m s - 1 (|r| <= 2^-10, one fma), log x = e' ln 2 + T + log1p(r), log1p by its degree-6
+// Taylor polynomial.  ~12 VALU and one 16-byte table read where fdlibm's reduction (a division)
+// takes ~25.  The two bins that touch y = 1 have c = 1, so near x = 1 the result is log1p(r) alone.
+__device__ __forceinline__ double log_tab(double x, const double2 *__restrict__ lt) {
+    const double m = __builtin_amdgcn_frexp_mant(x);
+    const int e = __builtin_amdgcn_frexp_exp(x);
+    const int i = (__double2hiint(m) >> 11) & 511;
+    const double2 st = lt[i];
+    const double r = fma(m, st.x, -1.0);
+    const double t = fma((double)(i < 256 ? e - 1 : e), 0x1.62e42fefa39efp-1, st.y);
+    double h = fma(r, -1.0 / 6.0, 0.2);
+    h = fma(r, h, -0.25);
+    h = fma(r, h, 1.0 / 3.0);
+    h = fma(r, h, -0.5);
+    return t + fma(r * r, h, r);
 }
 
 // phi of the scale-invariant kernels from the squared distance d2 = r^2 (scipy's
 // _rbfinterp_pythran forms up to rounding: the thin-plate spline as d2 log(d2) / 2, which needs no
 // square root; r^3 = d2 r, -r^5 = -(d2 d2) r).  A few ulps from scipy's r**2*log(r), far inside
 // what the solve amplifies (cond <= ~1e7 for these systems: 1e-9 relative at worst, 1e-13 typical).
-__device__ __forceinline__ double phi_ns(int kern, double d2) {
+template <int KERN>
+__device__ __forceinline__ double phi_ns_t(double d2, const double2 *__restrict__ lt) {
+    if constexpr (KERN == PTV_RBF_THIN_PLATE_SPLINE) return d2 == 0.0 ? 0.0 : (0.5 * d2) * log_tab(d2, lt);
+    if constexpr (KERN == PTV_RBF_CUBIC) return d2 * sqrt_spd(d2);
+    if constexpr (KERN == PTV_RBF_QUINTIC) return -((d2 * d2) * sqrt_spd(d2));
+    return -sqrt_spd(d2);  // linear
+}
+__device__ __forceinline__ double phi_ns(int kern, double d2, const double2 *__restrict__ lt) {
     switch (kern) {
-        case PTV_RBF_THIN_PLATE_SPLINE: return d2 == 0.0 ? 0.0 : (0.5 * d2) * log_ns(d2);
-        case PTV_RBF_CUBIC: return d2 * sqrt_spd(d2);
-        case PTV_RBF_QUINTIC: return -((d2 * d2) * sqrt_spd(d2));
-        default: return -sqrt_spd(d2);  // linear
+        case PTV_RBF_THIN_PLATE_SPLINE: return phi_ns_t<PTV_RBF_THIN_PLATE_SPLINE>(d2, lt);
+        case PTV_RBF_CUBIC: return phi_ns_t<PTV_RBF_CUBIC>(d2, lt);
+        case PTV_RBF_QUINTIC: return phi_ns_t<PTV_RBF_QUINTIC>(d2, lt);
+        default: return phi_ns_t<PTV_RBF_LINEAR>(d2, lt);
     }
 }
+
+// The symmetric build's phi entries: the NC x H (row i, column (i + d) mod NC) entries as one list
+// dealt round-robin over the 16 lanes of a system (ceil(NC H / 16) phi per lane: 13 at 20 slots, 18
+// at 24, where one row per lane-set costs R H = 20, 24), each written where the read-back finds it
+// (the full matrix, or NsBuild's half scheme).  One instantiation per kernel function, the loop
+// unrolled by 4 so that independent phi chains (and their LDS loads) overlap.
+template <int KERN, int NC, bool FULL>
+__device__ __forceinline__ void ns_build(double *__restrict__ ss, const double4 *__restrict__ ye, int li, int k,
+                                         const double2 *__restrict__ lt) {
+    using Bd = NsBuild<NC>;
+    constexpr int H = Bd::H, MS = NC + 1;
+    constexpr int NSLOT = NC * H;
+    constexpr int SPL = (NSLOT + 15) / 16;
+    static_assert(NC >= 16, "at most one wrap of the row index per step");
+    int i = li, dd = 1;  // entry p = sl * 16 + li is (row i, column (i + dd) mod NC), p = (dd - 1) NC + i
+#pragma unroll 4
+    for (int sl = 0; sl < SPL; ++sl, i += 16, dd += i >= NC ? 1 : 0, i -= i >= NC ? NC : 0) {
+        if (NSLOT % 16 == 0 || sl * 16 + li < NSLOT) {
+            int j = i + dd;
+            j -= j >= NC ? NC : 0;
+            double e = 0.0;
+            if (i < k && j < k) {
+                const double4 yv = ye[i], yj = ye[j];
+                const double dx = yv.x - yj.x, dy = yv.y - yj.y, dz = yv.z - yj.z;
+                e = phi_ns_t<KERN>((dx * dx + dy * dy) + dz * dz, lt);
+            }
+            if constexpr (FULL) {
+                ss[i * MS + j] = e;
+                ss[j * MS + i] = e;
+            } else {
+                ss[Bd::addr(i, dd - 1)] = e;
+            }
+        }
+    }
+}
+
+// rank[q] += #{sources j >= J: id_j < id[q]}, source j = lane j % 16 of row set j / 16 (row_newbcast)
+template <int J, int NC, int R>
+__device__ __forceinline__ void ns_rank(const uint32_t (&id)[R], int (&rank)[R]) {
+    if constexpr (J < NC) {
+        const uint32_t o = dpp_u32<0x150 + (J & 15)>(id[J >> 4]);
+#pragma unroll
+        for (int q = 0; q < R; ++q) rank[q] += o < id[q] ? 1 : 0;
+        ns_rank<J + 1, NC, R>(id, rank);
+    }
+}
+
+// one neighbour's particle record: position, velocity, index (zeros when not loaded)
+// (loaded unconditionally from an in-range slot and selected where used: a load under a branch
+// makes the compiler copy its result at the branch's end, which waits for every load in flight)
+struct NsRec {
+    double x, y, z, id, u, v, w;
+};
+__device__ __forceinline__ NsRec ns_rec(const double4 *__restrict__ prec, const double4 *__restrict__ pval,
+                                        uint32_t sl) {
+    const double4 p = prec[sl];
+    const double *q = reinterpret_cast<const double *>(pval + sl);
+    return NsRec{p.x, p.y, p.z, p.w, q[0], q[1], q[2]};
+}
+__device__ uint8_t kNsMaskOn = 1;  // the mask byte read when there is no mask (global, not flat)
 
 template <int NC, int NP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_rbf_ns(
@@ -206,31 +287,95 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     constexpr bool FULL = NC <= 20;
     constexpr int MS = NC + 1;
     constexpr int SCS = FULL ? 4 * NC * MS : 4 * NC * Bd::HS;
-    constexpr int SVS = 4 * NC * 8 + 4 * NC / 2;  // sorted (values, yhat) double4 pairs + ids per wave
+    constexpr int SVS = 4 * NC * 8;  // sorted (values, yhat) double4 pairs per wave
     constexpr int SRS = NP * R * 64 + 4 * 2 * NP;   // reflectors (per lane) + tau, beta (per system)
     constexpr int SC0 = SCS > SVS ? SCS : SVS;
     constexpr int SC = SC0 > SRS ? SC0 : SRS;
     __shared__ double4 s_ye[4][4][NC];  // per wave and system: eps-scaled coordinates + id, id order
     __shared__ double s_sc[4][SC];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    // the log's reduction table: in LDS up to 24 slots (8 KB; two blocks per CU still fit), read
+    // from global memory (L1) at 32, where the two blocks' scratch takes the whole LDS
+    constexpr bool LDS_LT = NC <= 24;
+    __shared__ double2 s_lt[LDS_LT ? 512 : 1];
+    const double2 *lt = reinterpret_cast<const double2 *>(kLogTab);
+    if constexpr (LDS_LT) {
+        for (int i = threadIdx.x; i < 512; i += 256) s_lt[i] = lt[i];
+        __syncthreads();
+        lt = s_lt;
+    }
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: the quad loop is scalar
+
+    const long long plane = (long long)a.nx * a.ny;
+    const long long nvox = (long long)(a.z1 - a.z0) * plane;
+    const int k = a.k;
+    const double eps = a.epsilon;
+    // Persistent waves, one quad (4 voxels, one per 16-lane system) at a time.  XCD-aware: block b
+    // runs on XCD b mod 8 (round-robin dispatch), and XCD x owns the contiguous eighth x of the
+    // quads, so the neighbourhoods one XCD gathers overlap in its own L2.  The next quad's slots
+    // and particle records are loaded while this one solves (slots after step 1, records after
+    // step 3): the gather latency that one quad per wave exposes (a quarter of the cycles) hides.
+    const long long nquad = (nvox + 3) / 4;
+    const int xcd = (int)(blockIdx.x & 7u);
+    const long long qend = nquad * (xcd + 1) / 8;
+    const long long qstep = (long long)(gridDim.x >> 3) * 4;
+    long long qd = nquad * xcd / 8 + (long long)(blockIdx.x >> 3) * 4 + wid;
+    // records in flight: 13 VGPRs per row slot; at 32 slots the solve leaves no room for them, and
+    // only the slots are prefetched (the records then load at the top of the quad)
+    constexpr bool PFR = NC <= 24;
+    uint32_t nsl[R];
+    NsRec nrec[R];
+    bool nvv;  // the next quad's voxel is in range
+    uint32_t nmb;  // its mask byte
+    int nz;
+    long long nrem;
+    double nq[3];
+    // the quad after this one: voxel (z plane, in-plane offset, coordinates), mask byte and slots,
+    // all loaded from in-range addresses without branches; validity applies where they are used
+    auto stage1 = [&](long long qn, int seg, int li) {
+        const long long vn = qn * 4 + seg;
+        nvv = qn < qend && vn < nvox;
+        const long long vc = nvv ? vn : nvox - 1;
+        nz = a.z0 + (int)(vc / plane);
+        nrem = vc - (long long)(nz - a.z0) * plane;
+        const int iy = (int)(nrem / a.nx), ix = (int)(nrem - (long long)iy * a.nx);
+        const size_t vfull = (size_t)nz * plane + nrem;
+        nmb = *(mask != nullptr ? mask + vfull : &kNsMaskOn);
+        const bool sep = a.separable != 0;
+        nq[0] = *(sep ? ax + ix : qpx + vfull);
+        nq[1] = *(sep ? ay + iy : qpy + vfull);
+        nq[2] = *(sep ? az + nz : qpz + vfull);
+#pragma unroll
+        for (int q = 0; q < R; ++q) nsl[q] = slots[(size_t)vc * k + (li + 16 * q < k ? li + 16 * q : k - 1)];
+    };
+    // stage 2 (or the top of the quad, without record prefetch): the records of the slots in use
+    auto stage2 = [&](int li) {
+        const bool act = nvv && nmb != 0u;
+#pragma unroll
+        for (int q = 0; q < R; ++q) nrec[q] = ns_rec(prec, pval, act && li + 16 * q < k ? nsl[q] : 0u);
+    };
+    int pwl;  // this lane's monomial exponents (lanes < NP), read once
+    {
+        const int seg = (threadIdx.x & 63) >> 4, li = threadIdx.x & 15;
+        pwl = pw[li < NP ? li : 0];
+        stage1(qd, seg, li);
+        if constexpr (PFR) stage2(li);
+    }
+    for (; qd < qend; qd += qstep) {
+    // the lane index re-derived opaquely each quad: nothing lane-dependent (the many LDS addresses
+    // of the unrolled steps) is hoisted out of the loop to stay live across the solve
+    int lane = threadIdx.x & 63;
+    asm volatile("" : "+v"(lane));
     const int seg = lane >> 4, li = lane & 15;
     double4 *ye = s_ye[wid][seg];
     double *sc = s_sc[wid];
     double4 *sv = reinterpret_cast<double4 *>(sc) + seg * NC * 2;  // row r: sv[2r] values, sv[2r+1] yhat
-    uint32_t *sid = reinterpret_cast<uint32_t *>(sc + 4 * NC * 8) + seg * NC;
-
-    const long long plane = (long long)a.nx * a.ny;
-    const long long nvox = (long long)(a.z1 - a.z0) * plane;
-    const long long v = ((long long)blockIdx.x * 4 + wid) * 4 + seg;  // chunk-local voxel
+    const long long v = qd * 4 + seg;  // chunk-local voxel
     const bool valid = v < nvox;
-    const long long vc = valid ? v : nvox - 1;
-    const int iz = a.z0 + (int)(vc / plane);
-    const long long rem = vc % plane;
-    const int iy = (int)(rem / a.nx), ix = (int)(rem % a.nx);
-    const size_t vfull = (size_t)iz * plane + rem;
-    const bool active = valid && (mask == nullptr || mask[vfull] != 0);
-    const int k = a.k;
-    const double eps = a.epsilon;
+    const int iz = nz;
+    const long long rem = nrem;
+    const bool active = nvv && nmb != 0u;
+    const double qx = nq[0], qy = nq[1], qz = nq[2];
+    if constexpr (!PFR) stage2(li);
 #if PTV_NS_STAMP
     unsigned long long ts[9];
 #endif
@@ -244,14 +389,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 #pragma unroll
     for (int q = 0; q < R; ++q) {
         const int nbr = li + 16 * q;
-        r[q] = make_double4(0.0, 0.0, 0.0, 0.0);
-        d[q] = r[q];
+        const bool ld = active && nbr < k;
+        r[q] = ld ? make_double4(nrec[q].x, nrec[q].y, nrec[q].z, 0.0) : make_double4(0.0, 0.0, 0.0, 0.0);
+        d[q] = ld ? make_double4(nrec[q].u, nrec[q].v, nrec[q].w, 0.0) : make_double4(0.0, 0.0, 0.0, 0.0);
         id[q] = 0xffffffffu;
-        if (active && nbr < k) {
-            const uint32_t sl = slots[(size_t)v * k + nbr];
-            r[q] = prec[sl];
-            d[q] = pval[sl];
-            id[q] = (uint32_t)r[q].w;
+        if (ld) {
+            id[q] = (uint32_t)nrec[q].id;
             mn[0] = fmin(mn[0], r[q].x);
             mn[1] = fmin(mn[1], r[q].y);
             mn[2] = fmin(mn[2], r[q].z);
@@ -259,56 +402,41 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
             mx[1] = fmax(mx[1], r[q].y);
             mx[2] = fmax(mx[2], r[q].z);
         }
-        if (nbr < NC) sid[nbr] = id[q];
     }
     double sh[3] = {0.0, 0.0, 0.0}, scl[3] = {1.0, 1.0, 1.0};
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         const double lo = seg_min<16>(mn[c]), hi = seg_max<16>(mx[c]);
         if (active) {
-            sh[c] = (hi + lo) / 2.0;
-            scl[c] = (hi - lo) / 2.0;
-            if (scl[c] == 0.0) scl[c] = 1.0;
+            sh[c] = (hi + lo) * 0.5;
+            scl[c] = (hi - lo) * 0.5;
+            scl[c] = scl[c] == 0.0 ? 1.0 : 1.0 / scl[c];  // kept as the reciprocal: yhat = (y - shift) * (1 / scale)
         }
     }
     // the voxel (x), and its monomial P_li(xhat) on lanes li < NP (evaluated at the end: computed
     // here so that neither the shift / scale nor the coordinates stay live through the solve)
-    double qx, qy, qz;
-    if (a.separable) {
-        qx = ax[ix];
-        qy = ay[iy];
-        qz = az[iz];
-    } else {
-        qx = qpx[vfull];
-        qy = qpy[vfull];
-        qz = qpz[vfull];
-    }
-    const double pm = li < NP ? mono2((qx - sh[0]) / scl[0], (qy - sh[1]) / scl[1], (qz - sh[2]) / scl[2],
-                                      pw[li < NP ? li : 0]) : 0.0;
-    rbf_wave_sync();
+    const double pm = li < NP ? mono2((qx - sh[0]) * scl[0], (qy - sh[1]) * scl[1], (qz - sh[2]) * scl[2],
+                                      pwl) : 0.0;
+    // rank = the number of smaller particle indices in the neighbourhood (the k slots hold distinct
+    // particles; unused slots hold 0xffffffff and count for nobody), each source broadcast by DPP
     int rank[R];
 #pragma unroll
     for (int q = 0; q < R; ++q) rank[q] = 0;
-    for (int j = 0; j < k; ++j) {
-        const uint32_t o = sid[j];
-#pragma unroll
-        for (int q = 0; q < R; ++q) rank[q] += (o < id[q] || (o == id[q] && j < li + 16 * q)) ? 1 : 0;
-    }
-    rbf_wave_sync();
+    ns_rank<0, NC, R>(id, rank);
 #pragma unroll
     for (int q = 0; q < R; ++q) {
         if (li + 16 * q < k) {
             ye[rank[q]] = make_double4(r[q].x * eps, r[q].y * eps, r[q].z * eps, (double)id[q]);
             sv[2 * rank[q]] = d[q];
-            sv[2 * rank[q] + 1] = make_double4((r[q].x - sh[0]) / scl[0], (r[q].y - sh[1]) / scl[1],
-                                               (r[q].z - sh[2]) / scl[2], 0.0);
+            sv[2 * rank[q] + 1] = make_double4((r[q].x - sh[0]) * scl[0], (r[q].y - sh[1]) * scl[1],
+                                               (r[q].z - sh[2]) * scl[2], 0.0);
         }
     }
     rbf_wave_sync();
     double4 yi[R], hh[R];  // own rows' eps-scaled coordinates (build only: reloaded for the evaluation), yhat
     double B[R][3], dg[R];
     bool bad = false;
-    const double phi0 = phi_ns(a.kernel, 0.0);
+    const double phi0 = phi_ns(a.kernel, 0.0, lt);
 #pragma unroll
     for (int q = 0; q < R; ++q) {
         const int row = li + 16 * q;
@@ -321,17 +449,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         B[q][2] = dv.z;
         double si = 0.0;
         if (kr && active) si = smooth != nullptr ? smooth[(size_t)yi[q].w] : a.smoothing;
+        // consumed here, before the next quad's loads issue: a later first use would wait for those too
+        asm volatile("" : "+v"(si));
         bad = bad || si < 0.0;  // negative smoothing: not positive definite any more
         dg[q] = kr ? phi0 + si : 1.0;  // padded rows: identity block
     }
-    // P rows: monomials of yhat (degree <= 2: exponents 0..2, the products of ipow's fast paths)
+    {  // prefetch, stage 1: the next quad's slots
+        stage1(qd + qstep, seg, li);
+    }
+    // P rows: monomials of yhat, exponents fixed by NP at compile time (kNsPow; unused rows have
+    // yhat = 0, so only the constant column needs the row test)
     double P[R][NP];
 #pragma unroll
-    for (int q = 0; q < R; ++q) {
-        const bool kr = li + 16 * q < k;
-#pragma unroll
-        for (int t = 0; t < NP; ++t) P[q][t] = kr ? mono2(hh[q].x, hh[q].y, hh[q].z, pw[t]) : 0.0;
-    }
+    for (int q = 0; q < R; ++q) ns_prow<0, NP>(P[q], hh[q], li + 16 * q < k);
     PTV_NS_MARK(1);
     // ---- 2. Householder QR of P alone (the reflectors depend on P only; dlarfg: beta = -sign(alpha)
     //      ||x||, tau = (beta - alpha)/beta, v = x / (alpha - beta), v_t = 1), applied to P's later
@@ -394,31 +524,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
             if (16 * q + 15 < NC || row < NC) ss[row * MS + row] = dg[q];
         }
     }
-    // the NC x H (row i, column (i + d) mod NC) entries as one list dealt round-robin over the 16
-    // lanes (ceil(NC H / 16) phi per lane: 13 at 20 slots, 18 at 24, where one row per lane-set
-    // costs R H = 20, 24), each written where the read-back finds it
-    constexpr int NSLOT = NC * H;
-    constexpr int SPL = (NSLOT + 15) / 16;
-#pragma unroll 1
-    for (int sl = 0; sl < SPL; ++sl) {
-        const int p = sl * 16 + li;
-        if (NSLOT % 16 == 0 || p < NSLOT) {
-            const int dd = p / NC + 1, i = p - (dd - 1) * NC;
-            int j = i + dd;
-            j -= j >= NC ? NC : 0;
-            double e = 0.0;
-            if (i < k && j < k) {
-                const double4 yv = ye[i], yj = ye[j];
-                const double dx = yv.x - yj.x, dy = yv.y - yj.y, dz = yv.z - yj.z;
-                e = phi_ns(a.kernel, (dx * dx + dy * dy) + dz * dz);
-            }
-            if constexpr (FULL) {
-                ss[i * MS + j] = e;
-                ss[j * MS + i] = e;
-            } else {
-                ss[Bd::addr(i, dd - 1)] = e;
-            }
-        }
+    switch (a.kernel) {
+        case PTV_RBF_THIN_PLATE_SPLINE: ns_build<PTV_RBF_THIN_PLATE_SPLINE, NC, FULL>(ss, ye, li, k, lt); break;
+        case PTV_RBF_CUBIC: ns_build<PTV_RBF_CUBIC, NC, FULL>(ss, ye, li, k, lt); break;
+        case PTV_RBF_QUINTIC: ns_build<PTV_RBF_QUINTIC, NC, FULL>(ss, ye, li, k, lt); break;
+        default: ns_build<PTV_RBF_LINEAR, NC, FULL>(ss, ye, li, k, lt);
     }
     rbf_wave_sync();
     PTV_NS_MARK(3);
@@ -457,6 +567,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // bounded reads in flight
     }
     rbf_wave_sync();  // every lane has its rows: the scratch now keeps the reflectors for step 8
+    if constexpr (PFR) stage2(li);  // prefetch, stage 2: the next quad's particle records
     double *vst = sc;                                  // V[t][q] at vst[(t * R + q) * 64 + lane]
     double *tbs = sc + NP * R * 64 + seg * (2 * NP);  // tau[t], beta[t] of this system
     static_assert(NP * R * 64 + 4 * 2 * NP <= SC, "reflector store fits the scratch");
@@ -626,7 +737,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         if (li + 16 * q < k) {
             const double4 y = ye[li + 16 * q];
             const double dx = qx * eps - y.x, dy = qy * eps - y.y, dz = qz * eps - y.z;
-            ph[q] = phi_ns(a.kernel, (dx * dx + dy * dy) + dz * dz);
+            ph[q] = phi_ns(a.kernel, (dx * dx + dy * dy) + dz * dz, lt);
         }
     }
 #pragma unroll
@@ -656,34 +767,51 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     PTV_NS_MARK(8);
 #if PTV_NS_STAMP
     if (a.stamps != nullptr && lane == 0) {
-        const long long gw = (long long)blockIdx.x * 4 + wid;
-        if (gw < a.stamp_cap)
-            for (int i = 0; i < 8; ++i) a.stamps[gw * 8 + i] = ts[i + 1] - ts[i];
+        if (qd < a.stamp_cap)
+            for (int i = 0; i < 8; ++i) a.stamps[qd * 8 + i] = ts[i + 1] - ts[i];
     }
 #endif
-    if (!valid || li != 0) return;
-    const size_t vo = (size_t)(iz - a.out_z0) * plane + rem;
-    if (!active) {
-        U[vo] = 0.0;
-        V[vo] = 0.0;
-        W[vo] = 0.0;
-        return;
-    }
-    if (segbad) {  // re-solved by the pivoting kernel (k_rbf_local over the list)
-        const int at = atomicAdd(&status[3], 1);
-        atomicAdd(&status[5], 1);
-        if (at < a.ns_cap) a.ns_list[at] = (uint32_t)v;
-        else atomicOr(&status[4], 1);
-        return;
-    }
-    if (a.flags & PTV_FLAG_NAN_TO_NUM) {
+    if (valid && li == 0) {
+        const size_t vo = (size_t)(iz - a.out_z0) * plane + rem;
+        if (!active) {
+            U[vo] = 0.0;
+            V[vo] = 0.0;
+            W[vo] = 0.0;
+        } else if (segbad) {  // re-solved by the pivoting kernel (k_rbf_local over the list)
+            const int at = atomicAdd(&status[3], 1);
+            atomicAdd(&status[5], 1);
+            if (at < a.ns_cap) a.ns_list[at] = (uint32_t)v;
+            else atomicOr(&status[4], 1);
+        } else {
+            if (a.flags & PTV_FLAG_NAN_TO_NUM) {
 #pragma unroll
-        for (int c = 0; c < 3; ++c)
-            o[c] = o[c] != o[c] ? 0.0 : (o[c] == INFINITY ? DBL_MAX : (o[c] == -INFINITY ? -DBL_MAX : o[c]));
+                for (int c = 0; c < 3; ++c)
+                    o[c] = o[c] != o[c] ? 0.0
+                                        : (o[c] == INFINITY ? DBL_MAX : (o[c] == -INFINITY ? -DBL_MAX : o[c]));
+            }
+            U[vo] = o[0];
+            V[vo] = o[1];
+            W[vo] = o[2];
+        }
     }
-    U[vo] = o[0];
-    V[vo] = o[1];
-    W[vo] = o[2];
+    rbf_wave_sync();  // the next quad reuses this wave's LDS
+    }  // quads
+}
+
+// persistent grid: the blocks one wave of residency holds (occupancy x CUs), a multiple of the 8
+// XCDs; a block that waited for a free CU would find its quads' share undone at the end
+inline unsigned ns_grid(long long nquad, int per_cu) {
+    static int cus[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    int c = __atomic_load_n(&cus[dev], __ATOMIC_RELAXED);
+    if (c <= 0) {
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+        __atomic_store_n(&cus[dev], c, __ATOMIC_RELAXED);
+    }
+    long long nb = (nquad + 3) / 4, cap = (long long)c * (per_cu > 0 ? per_cu : 1);
+    if (nb > cap) nb = cap;
+    return (unsigned)((nb + 7) / 8 * 8);
 }
 
 template <int NC, int NP>
@@ -691,8 +819,15 @@ void launch_ns_t(const RbfKernelArgs &ka, long long nvox, hipStream_t s, const d
                  const uint32_t *slots, const double *ax, const double *ay, const double *az, const double *qx,
                  const double *qy, const double *qz, const double *smooth, const int *pw, const uint8_t *mask,
                  double *U, double *V, double *W, int *status) {
-    const long long waves = (nvox + 3) / 4;
-    hipLaunchKernelGGL((k_rbf_ns<NC, NP>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, ka, prec, pval, slots,
+    static int occ = 0;
+    int per_cu = __atomic_load_n(&occ, __ATOMIC_RELAXED);
+    if (per_cu <= 0) {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_rbf_ns<NC, NP>, 256, 0) != hipSuccess ||
+            per_cu <= 0)
+            per_cu = 1;
+        __atomic_store_n(&occ, per_cu, __ATOMIC_RELAXED);
+    }
+    hipLaunchKernelGGL((k_rbf_ns<NC, NP>), dim3(ns_grid((nvox + 3) / 4, per_cu)), dim3(256), 0, s, ka, prec, pval, slots,
                        ax, ay, az, qx, qy, qz, smooth, pw, mask, U, V, W, status);
 }
 
