@@ -1084,7 +1084,8 @@ static bool rbf_ns(const RbfKernelArgs &ka, const double *smooth, long long nvox
     const int np = ka.m - ka.k;
     if (!(np == 1 || np == 4 || (np == 10 && ka.k <= 24))) return false;
     if (ka.k <= np || ka.k > 32) return false;
-    if (smooth == nullptr && !(ka.smoothing >= 0.0)) return false;
+    // scalar smoothing the kernel would flag on every voxel (negative, or > 2^26: k_rbf_ns step 1)
+    if (smooth == nullptr && !(ka.smoothing >= 0.0 && ka.smoothing <= 0x1p26)) return false;
     const int degree = np == 1 ? 0 : (np == 4 ? 1 : 2);
     switch (ka.kernel) {
         case PTV_RBF_LINEAR: return degree >= 0;             // -r: order 1

@@ -194,7 +194,8 @@ __device__ __forceinline__ double log_tab(double x, const double2 *__restrict__ 
 // what the solve amplifies (cond <= ~1e7 for these systems: 1e-9 relative at worst, 1e-13 typical).
 template <int KERN>
 __device__ __forceinline__ double phi_ns_t(double d2, const double2 *__restrict__ lt) {
-    if constexpr (KERN == PTV_RBF_THIN_PLATE_SPLINE) return d2 == 0.0 ? 0.0 : (0.5 * d2) * log_tab(d2, lt);
+    // log_tab(0) is finite (m = 0: r = -1), so d2 = 0 gives 0 with no test
+    if constexpr (KERN == PTV_RBF_THIN_PLATE_SPLINE) return (0.5 * d2) * log_tab(d2, lt);
     if constexpr (KERN == PTV_RBF_CUBIC) return d2 * sqrt_spd(d2);
     if constexpr (KERN == PTV_RBF_QUINTIC) return -((d2 * d2) * sqrt_spd(d2));
     return -sqrt_spd(d2);  // linear
@@ -222,17 +223,17 @@ __device__ __forceinline__ void ns_build(double *__restrict__ ss, const double4 
     constexpr int SPL = (NSLOT + 15) / 16;
     static_assert(NC >= 16, "at most one wrap of the row index per step");
     int i = li, dd = 1;  // entry p = sl * 16 + li is (row i, column (i + dd) mod NC), p = (dd - 1) NC + i
-#pragma unroll 4
+    // branch-free, fully unrolled (the entries' LDS reads and phi chains overlap): rows >= k hold
+    // stale coordinates, their phi is computed and dropped
+#pragma unroll
     for (int sl = 0; sl < SPL; ++sl, i += 16, dd += i >= NC ? 1 : 0, i -= i >= NC ? NC : 0) {
-        if (NSLOT % 16 == 0 || sl * 16 + li < NSLOT) {
+        if (NSLOT % 16 == 0 || sl + 1 < SPL || sl * 16 + li < NSLOT) {
             int j = i + dd;
             j -= j >= NC ? NC : 0;
-            double e = 0.0;
-            if (i < k && j < k) {
-                const double4 yv = ye[i], yj = ye[j];
-                const double dx = yv.x - yj.x, dy = yv.y - yj.y, dz = yv.z - yj.z;
-                e = phi_ns_t<KERN>((dx * dx + dy * dy) + dz * dz, lt);
-            }
+            const double4 yv = ye[i], yj = ye[j];
+            const double dx = yv.x - yj.x, dy = yv.y - yj.y, dz = yv.z - yj.z;
+            const double ph = phi_ns_t<KERN>((dx * dx + dy * dy) + dz * dz, lt);
+            const double e = i < k && j < k ? ph : 0.0;
             if constexpr (FULL) {
                 ss[i * MS + j] = e;
                 ss[j * MS + i] = e;
@@ -410,7 +411,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         if (active) {
             sh[c] = (hi + lo) * 0.5;
             scl[c] = (hi - lo) * 0.5;
-            scl[c] = scl[c] == 0.0 ? 1.0 : 1.0 / scl[c];  // kept as the reciprocal: yhat = (y - shift) * (1 / scale)
+            scl[c] = scl[c] == 0.0 ? 1.0 : rcp_nr(scl[c]);  // kept as the reciprocal: yhat = (y - shift) * (1 / scale)
         }
     }
     // the voxel (x), and its monomial P_li(xhat) on lanes li < NP (evaluated at the end: computed
@@ -451,7 +452,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         if (kr && active) si = smooth != nullptr ? smooth[(size_t)yi[q].w] : a.smoothing;
         // consumed here, before the next quad's loads issue: a later first use would wait for those too
         asm volatile("" : "+v"(si));
-        bad = bad || si < 0.0;  // negative smoothing: not positive definite any more
+        // negative smoothing: not positive definite any more; smoothing far above the phi entries'
+        // scale (> 2^26): the rank-2r update then cancels the O(1) entries against it, inaccurately
+        // and without a telltale pivot (2e307 on every fifth diagonal left one wrong voxel in 1000)
+        bad = bad || si < 0.0 || si > 0x1p26;
         dg[q] = kr ? phi0 + si : 1.0;  // padded rows: identity block
     }
     {  // prefetch, stage 1: the next quad's slots
@@ -481,9 +485,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         const double nrm = sqrt(alpha * alpha + s);
         const bool triv = !(s > 0.0);
         const double b = triv ? alpha : (alpha >= 0.0 ? -nrm : nrm);
-        tau[t] = triv ? 0.0 : (b - alpha) / b;
+        // Newton reciprocals (a column this small is flagged rank-deficient below and re-solved)
+        tau[t] = triv ? 0.0 : (b - alpha) * rcp_nr(b);
         beta[t] = b;
-        const double scal = triv ? 0.0 : 1.0 / (alpha - b);
+        const double scal = triv ? 0.0 : rcp_nr(alpha - b);
         bad = bad || !(fabs(b) >= rank_tol);
 #pragma unroll
         for (int q = 0; q < R; ++q) {
@@ -719,7 +724,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     double E[3] = {0.0, 0.0, 0.0}, rh[3] = {B[0][0], B[0][1], B[0][2]};
 #pragma unroll
     for (int t = NP - 1; t >= 0; --t) {
-        const double rbt = 1.0 / tbs[NP + t];
+        const double rbt = rcp_nr(tbs[NP + t]);
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             const double et = rowbcast_n(t, rh[c] * rbt);
@@ -732,13 +737,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     // ---- 8. evaluate: out = (Q^T phi(x))[r:] . c~2 + P(xhat) . e ----
     double ph[R];
 #pragma unroll
-    for (int q = 0; q < R; ++q) {
-        ph[q] = 0.0;
-        if (li + 16 * q < k) {
-            const double4 y = ye[li + 16 * q];
-            const double dx = qx * eps - y.x, dy = qy * eps - y.y, dz = qz * eps - y.z;
-            ph[q] = phi_ns(a.kernel, (dx * dx + dy * dy) + dz * dz, lt);
-        }
+    for (int q = 0; q < R; ++q) {  // branch-free: slots past k (stale coordinates) are dropped
+        const int row = li + 16 * q;
+        const double4 y = ye[16 * q + 15 < NC || row < NC ? row : row - 16];
+        const double dx = qx * eps - y.x, dy = qy * eps - y.y, dz = qz * eps - y.z;
+        const double f = phi_ns(a.kernel, (dx * dx + dy * dy) + dz * dz, lt);
+        ph[q] = row < k ? f : 0.0;
     }
 #pragma unroll
     for (int t = 0; t < NP; ++t) {
