@@ -79,12 +79,6 @@ __device__ __forceinline__ void ns_prow(double (&row)[NP], const double4 &h, boo
     }
 }
 
-// x ** p for p in 0..2, as ipow (ptv_rbf_math.hpp) computes them, branch-free
-__device__ __forceinline__ double ipow2(double x, int p) { return p == 0 ? 1.0 : (p == 1 ? x : x * x); }
-// monomial with exponents packed as px | py << 8 | pz << 16, each <= 2 (degree <= 2)
-__device__ __forceinline__ double mono2(double hx, double hy, double hz, int code) {
-    return (ipow2(hx, code & 255) * ipow2(hy, (code >> 8) & 255)) * ipow2(hz, code >> 16);
-}
 
 
 // ---- v_fmac_f64 with its first operand broadcast from lane N of the 16-lane row (gfx950 DPALU
@@ -278,6 +272,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     const uint8_t *__restrict__ mask, double *__restrict__ U, double *__restrict__ V, double *__restrict__ W,
     int *__restrict__ status) {
     static_assert(NC % 4 == 0 && NC >= 16 && NC <= 32, "row slots");
+    (void)pw;  // the exponents are fixed by NP (kNsPow)
     static_assert(NP >= 1 && NP < 16 && NP < NC, "polynomial terms (rows 0..NP-1 in lanes 0..NP-1)");
     constexpr int R = (NC + 15) / 16;
     using Bd = NsBuild<NC>;
@@ -336,9 +331,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         const long long vn = qn * 4 + seg;
         nvv = qn < qend && vn < nvox;
         const long long vc = nvv ? vn : nvox - 1;
-        nz = a.z0 + (int)(vc / plane);
-        nrem = vc - (long long)(nz - a.z0) * plane;
-        const int iy = (int)(nrem / a.nx), ix = (int)(nrem - (long long)iy * a.nx);
+        // 32-bit divisions (the launch has <= 2^32 voxels, so the offsets fit; one plane of exactly
+        // 2^32 voxels takes the 64-bit branch, uniform)
+        uint32_t pz, pr;
+        if (plane <= 0xffffffffLL) {
+            const uint32_t v32 = (uint32_t)vc, p32 = (uint32_t)plane;
+            pz = v32 / p32;
+            pr = v32 - pz * p32;
+        } else {
+            pz = (uint32_t)(vc / plane);
+            pr = (uint32_t)(vc - (long long)pz * plane);
+        }
+        nz = a.z0 + (int)pz;
+        nrem = pr;
+        const uint32_t iyu = pr / (uint32_t)a.nx;
+        const int iy = (int)iyu, ix = (int)(pr - iyu * (uint32_t)a.nx);
         const size_t vfull = (size_t)nz * plane + nrem;
         nmb = *(mask != nullptr ? mask + vfull : &kNsMaskOn);
         const bool sep = a.separable != 0;
@@ -354,13 +361,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 #pragma unroll
         for (int q = 0; q < R; ++q) nrec[q] = ns_rec(prec, pval, act && li + 16 * q < k ? nsl[q] : 0u);
     };
-    int pwl;  // this lane's monomial exponents (lanes < NP), read once
     {
         const int seg = (threadIdx.x & 63) >> 4, li = threadIdx.x & 15;
-        pwl = pw[li < NP ? li : 0];
         stage1(qd, seg, li);
         if constexpr (PFR) stage2(li);
     }
+    // a quad's outputs are stored after the next quad's records are in use: stores count in vmcnt,
+    // and stored right away they would hold up the wait for those records at the top of the loop
+    bool pend = false;
+    size_t pvo = 0;
+    double po[3] = {0.0, 0.0, 0.0};
+    auto flush = [&]() {
+        if (pend) {
+            U[pvo] = po[0];
+            V[pvo] = po[1];
+            W[pvo] = po[2];
+        }
+        pend = false;
+    };
     for (; qd < qend; qd += qstep) {
     // the lane index re-derived opaquely each quad: nothing lane-dependent (the many LDS addresses
     // of the unrolled steps) is hoisted out of the loop to stay live across the solve
@@ -383,10 +401,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     PTV_NS_MARK(0);
 
     // ---- 1. neighbours li + 16 q, ranked by particle index (np.sort(yindices), _rbfinterp.py:521);
-    //      shift / scale of the neighbourhood (_build_system: (max + min)/2, (max - min)/2, 0 -> 1) ----
+    //      the polynomial coordinates' scale ----
     double4 r[R], d[R];
     uint32_t id[R];
-    double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    double ro = 0.0;  // max-norm offset of this lane's neighbours from the voxel
 #pragma unroll
     for (int q = 0; q < R; ++q) {
         const int nbr = li + 16 * q;
@@ -396,28 +414,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         id[q] = 0xffffffffu;
         if (ld) {
             id[q] = (uint32_t)nrec[q].id;
-            mn[0] = fmin(mn[0], r[q].x);
-            mn[1] = fmin(mn[1], r[q].y);
-            mn[2] = fmin(mn[2], r[q].z);
-            mx[0] = fmax(mx[0], r[q].x);
-            mx[1] = fmax(mx[1], r[q].y);
-            mx[2] = fmax(mx[2], r[q].z);
+            ro = fmax(ro, fmax(fabs(r[q].x - qx), fmax(fabs(r[q].y - qy), fabs(r[q].z - qz))));
         }
     }
-    double sh[3] = {0.0, 0.0, 0.0}, scl[3] = {1.0, 1.0, 1.0};
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        const double lo = seg_min<16>(mn[c]), hi = seg_max<16>(mx[c]);
-        if (active) {
-            sh[c] = (hi + lo) * 0.5;
-            scl[c] = (hi - lo) * 0.5;
-            scl[c] = scl[c] == 0.0 ? 1.0 : rcp_nr(scl[c]);  // kept as the reciprocal: yhat = (y - shift) * (1 / scale)
-        }
-    }
-    // the voxel (x), and its monomial P_li(xhat) on lanes li < NP (evaluated at the end: computed
-    // here so that neither the shift / scale nor the coordinates stay live through the solve)
-    const double pm = li < NP ? mono2((qx - sh[0]) * scl[0], (qy - sh[1]) * scl[1], (qz - sh[2]) * scl[2],
-                                      pwl) : 0.0;
+    flush();  // the previous quad's outputs, now that this quad's records are in registers
+    // The polynomial block's coordinates: yhat = (y - x) / rho, centred on the voxel x and scaled by
+    // the neighbourhood's max-norm radius rho (in [-1, 1]^3).  scipy centres and scales per axis on
+    // the neighbourhood's box (_build_system); the polynomials of degree <= d span the same space
+    // under any affine change of coordinates, so the interpolant is the same up to rounding, and
+    // the null-space basis Q of P (its span) does not depend on the column scaling at all.  One
+    // reduction where the box takes six, and P(xhat) at the voxel is (1, 0, ..., 0).
+    const double rho = seg_max<16>(ro);
+    const double irho = rho > 0.0 ? rcp_nr(rho) : 1.0;
+    const double pm = li == 0 ? 1.0 : 0.0;
     // rank = the number of smaller particle indices in the neighbourhood (the k slots hold distinct
     // particles; unused slots hold 0xffffffff and count for nobody), each source broadcast by DPP
     int rank[R];
@@ -429,8 +438,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         if (li + 16 * q < k) {
             ye[rank[q]] = make_double4(r[q].x * eps, r[q].y * eps, r[q].z * eps, (double)id[q]);
             sv[2 * rank[q]] = d[q];
-            sv[2 * rank[q] + 1] = make_double4((r[q].x - sh[0]) * scl[0], (r[q].y - sh[1]) * scl[1],
-                                               (r[q].z - sh[2]) * scl[2], 0.0);
+            sv[2 * rank[q] + 1] = make_double4((r[q].x - qx) * irho, (r[q].y - qy) * irho, (r[q].z - qz) * irho, 0.0);
         }
     }
     rbf_wave_sync();
@@ -776,30 +784,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     }
 #endif
     if (valid && li == 0) {
-        const size_t vo = (size_t)(iz - a.out_z0) * plane + rem;
-        if (!active) {
-            U[vo] = 0.0;
-            V[vo] = 0.0;
-            W[vo] = 0.0;
-        } else if (segbad) {  // re-solved by the pivoting kernel (k_rbf_local over the list)
+        if (active && segbad) {  // re-solved by the pivoting kernel (k_rbf_local over the list)
             const int at = atomicAdd(&status[3], 1);
             atomicAdd(&status[5], 1);
             if (at < a.ns_cap) a.ns_list[at] = (uint32_t)v;
             else atomicOr(&status[4], 1);
-        } else {
+        } else {  // the output (zeros for a masked voxel), stored at the top of the next quad
             if (a.flags & PTV_FLAG_NAN_TO_NUM) {
 #pragma unroll
                 for (int c = 0; c < 3; ++c)
                     o[c] = o[c] != o[c] ? 0.0
                                         : (o[c] == INFINITY ? DBL_MAX : (o[c] == -INFINITY ? -DBL_MAX : o[c]));
             }
-            U[vo] = o[0];
-            V[vo] = o[1];
-            W[vo] = o[2];
+            pend = true;
+            pvo = (size_t)(iz - a.out_z0) * plane + rem;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) po[c] = active ? o[c] : 0.0;
         }
     }
     rbf_wave_sync();  // the next quad reuses this wave's LDS
     }  // quads
+    flush();
 }
 
 // persistent grid: the blocks one wave of residency holds (occupancy x CUs), a multiple of the 8

@@ -18,6 +18,9 @@ run headline 300
 run nearest 300 --method nearest --no-e2e
 run sibson 300 --method sibson --k 30 --no-e2e
 run idw_k50 400 --method idw --k 50 --steps 5 --warmup 1 --no-e2e
+run sibson_k50 400 --method sibson --k 50 --steps 5 --warmup 1 --no-e2e
+run rbf_tps20 600 --method rbf --k 20 --steps 3 --warmup 1
+run rbf_tps32 600 --method rbf --k 32 --steps 3 --warmup 1
 run c2 300 --config c2
 run c2r 300 --config c2r
 run c3 600 --config c3
