@@ -235,6 +235,12 @@ def row_traffic(*keys):
         return None
 
 
+def emit_line(line):
+    """Print one bench JSON line, stamped with the SHA-256 prefix of the library that ran it."""
+    line.setdefault("lib_sha256", lib_sha256())
+    print(json.dumps(line), flush=True)
+
+
 def lib_sha256():
     """First 16 hex digits of the loaded library's SHA-256 (tools/traffic.py records the same)."""
     import hashlib
@@ -784,7 +790,7 @@ def main_interp(args):
             line["allgather_ms"] = round(gather_ms, 2) if isinstance(gather_ms, float) else gather_ms
         if e2e is not None:
             line["e2e"] = e2e
-        print(json.dumps(line), flush=True)
+        emit_line(line)
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
@@ -888,7 +894,7 @@ def main_div(args):
                          "alg_bytes_per_launch": alg, "kernel_ms": round(kavg, 4)},
             "cpu_baseline": cpu,
         }
-        print(json.dumps(line), flush=True)
+        emit_line(line)
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
@@ -944,7 +950,7 @@ def main_filter(args):
         except Exception as e:
             cpu = {"value": None, "error": repr(e)[:200]}
     if rank == 0:
-        print(json.dumps({
+        emit_line({
             "metric": METRIC_FILTER, "value": round(n * world / (elapsed / args.steps) / 1e6, 2),
             "unit": "Mparticles/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
@@ -959,7 +965,7 @@ def main_filter(args):
                          if (k == 25 and n == 5_000_000) else None,
                          "kernel": f"k_knn_interp<{kmax_for(k + 1)}, filter> ((k+1)-NN + fused median/MAD)",
                          "alg_bytes_per_launch": alg, "kernel_ms": round(kavg, 4)},
-            "cpu_baseline": cpu}), flush=True)
+            "cpu_baseline": cpu})
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
@@ -1034,7 +1040,7 @@ def main_mask(args):
         except Exception as ex:
             cpu = {"value": None, "error": repr(ex)[:200]}
     if rank == 0:
-        print(json.dumps({
+        emit_line({
             "metric": METRIC_MASK, "value": round(V * world / (elapsed / args.steps) / 1e6, 2),
             "unit": "Mvoxels/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
@@ -1052,7 +1058,7 @@ def main_mask(args):
                          "alg_bytes_per_launch": alg_b, "kernel_ms": round(t_b, 4),
                          "sample_mask": {"achieved": round(ach_s, 1), "frac": round(ach_s / HBM_PEAK_GBPS, 4),
                                          "alg_bytes": alg_s, "kernel_ms": round(t_s, 4)}},
-            "cpu_baseline": cpu}), flush=True)
+            "cpu_baseline": cpu})
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
@@ -1123,7 +1129,7 @@ def main_linear(args):
         except Exception as e:
             cpu = {"value": None, "error": repr(e)[:200]}
     if rank == 0:
-        print(json.dumps({
+        emit_line({
             "metric": METRIC_LINEAR, "value": round(V * world / (elapsed / args.steps) / 1e6, 2),
             "unit": "Mvoxels/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
@@ -1139,7 +1145,7 @@ def main_linear(args):
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None, "kernel": "k_linear_walk",
                          "alg_bytes_per_launch": alg, "kernel_ms": round(wavg, 4)},
-            "cpu_baseline": cpu}), flush=True)
+            "cpu_baseline": cpu})
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
