@@ -30,8 +30,8 @@ ARCH = os.environ.get("PTV_OFFLOAD_ARCH", "gfx950")
 EXTRA = {f: ["-mllvm", "-pragma-unroll-threshold=1000000"] for f in ["ptv_rbf.hip"] + ["ptv_rbf_ns_" + g + ".hip" for g in "abcd"]}
 # the null-space kernel's persistent quad loop: machine LICM would hoist every VGPR constant (the
 # log polynomial, LDS offsets) out of it, live across the whole solve (~30 VGPRs, spills at 32 slots)
-for _g in "abcd":
-    EXTRA["ptv_rbf_ns_" + _g + ".hip"] += ["-mllvm", "-disable-machine-licm"]
+for _f in ["ptv_rbf.hip"] + ["ptv_rbf_ns_" + g + ".hip" for g in "abcd"]:  # k_rbf_spd16 loops the same way
+    EXTRA[_f] += ["-mllvm", "-disable-machine-licm"]
 
 COMMON = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", f"--offload-arch={ARCH}",
           "-I", INCLUDE, "-I", CSRC, "-Wno-unused-result"]

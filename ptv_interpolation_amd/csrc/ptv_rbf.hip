@@ -773,25 +773,86 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     // per SIMD) per CU
     constexpr int SC = 4 * (16 * R) * (8 * R) > 4 * 32 * 4 + 4 * 32 / 2 ? 4 * (16 * R) * (8 * R) : 4 * 32 * 4 + 4 * 32 / 2;
     __shared__ double s_sc[4][SC];  // (80 KB per block with s_ye: two blocks per CU, not a byte more)
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: the quad loop is scalar
+    const long long plane = (long long)a.nx * a.ny;
+    const long long nvox = (long long)(a.z1 - a.z0) * plane;
+    const int k = a.k;
+    const double eps = a.epsilon;
+    // Persistent, XCD-aware quads (4 voxels, one per 16-lane system) with the next quad's slots,
+    // mask byte and coordinates loaded after step 1 and its particle records after the read-back
+    // (k_rbf_ns does the same; the arithmetic of a quad is unchanged: bit-identical to k_rbf_spd)
+    const long long nquad = (nvox + 3) / 4;
+    const int xcd = (int)(blockIdx.x & 7u);
+    const long long qend = nquad * (xcd + 1) / 8;
+    const long long qstep = (long long)(gridDim.x >> 3) * 4;
+    long long qd = nquad * xcd / 8 + (long long)(blockIdx.x >> 3) * 4 + wid;
+    uint32_t nsl[R];
+    double4 nr[R], nd[R];
+    bool nvv;
+    uint32_t nmb;
+    int nz;
+    long long nrem;
+    double nq[3];
+    auto stage1 = [&](long long qn, int seg, int li) {
+        const long long vn = qn * 4 + seg;
+        nvv = qn < qend && vn < nvox;
+        const long long vc = nvv ? vn : nvox - 1;
+        nz = a.z0 + (int)(vc / plane);
+        nrem = vc - (long long)(nz - a.z0) * plane;
+        const int iy = (int)(nrem / a.nx), ix = (int)(nrem - (long long)iy * a.nx);
+        const size_t vfull = (size_t)nz * plane + nrem;
+        nmb = *(mask != nullptr ? mask + vfull : &kNsMaskOn);
+        const bool sep = a.separable != 0;
+        nq[0] = *(sep ? ax + ix : qpx + vfull);
+        nq[1] = *(sep ? ay + iy : qpy + vfull);
+        nq[2] = *(sep ? az + nz : qpz + vfull);
+#pragma unroll
+        for (int q = 0; q < R; ++q) nsl[q] = slots[(size_t)vc * k + (li + 16 * q < k ? li + 16 * q : k - 1)];
+    };
+    auto stage2 = [&](int li) {
+        const bool act = nvv && nmb != 0u;
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const uint32_t sl = act && li + 16 * q < k ? nsl[q] : 0u;
+            nr[q] = prec[sl];
+            nd[q] = pval[sl];
+        }
+    };
+    // records in flight cost 16 VGPRs per row set: at 32 rows the elimination leaves no room, and
+    // only the slots are prefetched (the records then load at the top of the quad)
+    constexpr bool PFR = M <= 24;
+    {
+        const int seg = (threadIdx.x & 63) >> 4, li = threadIdx.x & 15;
+        stage1(qd, seg, li);
+        if constexpr (PFR) stage2(li);
+    }
+    bool pend = false;  // a quad's outputs are stored once the next quad's records are in use
+    size_t pvo = 0;
+    double po[3] = {0.0, 0.0, 0.0};
+    auto flush = [&]() {
+        if (pend) {
+            U[pvo] = po[0];
+            V[pvo] = po[1];
+            W[pvo] = po[2];
+        }
+        pend = false;
+    };
+    for (; qd < qend; qd += qstep) {
+    int lane = threadIdx.x & 63;
+    asm volatile("" : "+v"(lane));  // nothing lane-dependent is hoisted out of the quad loop
     const int seg = lane >> 4, li = lane & 15;
     double4 *ye = s_ye[wid][seg];
     double *sc = s_sc[wid];
     double4 *sv = reinterpret_cast<double4 *>(sc) + seg * 32;
     uint32_t *sid = reinterpret_cast<uint32_t *>(sc + 4 * 32 * 4) + seg * 32;
-
-    const long long plane = (long long)a.nx * a.ny;
-    const long long nvox = (long long)(a.z1 - a.z0) * plane;
-    const long long v = ((long long)blockIdx.x * 4 + wid) * 4 + seg;  // chunk-local voxel
+    const long long v = qd * 4 + seg;  // chunk-local voxel
     const bool valid = v < nvox;
-    const long long vc = valid ? v : nvox - 1;
-    const int iz = a.z0 + (int)(vc / plane);
-    const long long rem = vc % plane;
-    const int iy = (int)(rem / a.nx), ix = (int)(rem % a.nx);
+    const int iz = nz;
+    const long long rem = nrem;
     const size_t vfull = (size_t)iz * plane + rem;
-    const bool active = valid && (mask == nullptr || mask[vfull] != 0);
-    const int k = a.k;
-    const double eps = a.epsilon;
+    const bool active = nvv && nmb != 0u;
+    const double qx = nq[0], qy = nq[1], qz = nq[2];
+    if constexpr (!PFR) stage2(li);
 
     // ---- 1. neighbours li and li + 16, ranked by particle index (np.sort(yindices)) ----
     double4 r[R], d[R];
@@ -799,17 +860,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 #pragma unroll
     for (int q = 0; q < R; ++q) {
         const int nbr = li + 16 * q;
-        r[q] = make_double4(0.0, 0.0, 0.0, 0.0);
-        d[q] = make_double4(0.0, 0.0, 0.0, 0.0);
-        id[q] = 0xffffffffu;
-        if (active && nbr < k) {
-            const uint32_t sl = slots[(size_t)v * k + nbr];
-            r[q] = prec[sl];
-            d[q] = pval[sl];
-            id[q] = (uint32_t)r[q].w;
-        }
+        const bool ld = active && nbr < k;
+        r[q] = ld ? nr[q] : make_double4(0.0, 0.0, 0.0, 0.0);
+        d[q] = ld ? nd[q] : make_double4(0.0, 0.0, 0.0, 0.0);
+        id[q] = ld ? (uint32_t)nr[q].w : 0xffffffffu;
         if (nbr < 32) sid[nbr] = id[q];
     }
+    flush();
     rbf_wave_sync();
     int rank[R];
 #pragma unroll
@@ -841,6 +898,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         B[q][2] = dv.z;
     }
     rbf_wave_sync();  // the values' LDS is the build scratch next
+    stage1(qd + qstep, seg, li);  // the next quad's slots, mask byte and coordinates
 
     // ---- 2. symmetric build of rows li and li + 16: row i evaluates phi for the columns
     //      (i + d) mod NR, d = 1..H, into a row-swizzled slot of its segment's scratch
@@ -849,19 +907,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     constexpr int NR = 16 * R, H = NR / 2;
     double *ss = sc + seg * (NR * H);
     const double diag = rbf_phi<KERN>(0.0) + a.smoothing;
-#pragma unroll 1
+    // branch-free and unrolled (the entries' LDS reads and phi chains overlap): slots past k hold
+    // stale coordinates, their phi is computed and dropped (same arithmetic as k_rbf_spd)
+#pragma unroll 4
     for (int dd = 1; dd <= H; ++dd) {
 #pragma unroll
         for (int q = 0; q < R; ++q) {
             const int row = li + 16 * q;
             const int j = (row + dd) & (NR - 1);
-            double e = 0.0;
-            if (row < k && j < k) {
-                const double4 yj = ye[j];
-                const double dx = yi[q].x - yj.x, dy = yi[q].y - yj.y, dz = yi[q].z - yj.z;
-                e = rbf_phi<KERN>(sqrt_spd((dx * dx + dy * dy) + dz * dz));
-            }
-            ss[row * H + ((dd - 1) ^ (row & (H - 1)))] = e;
+            const double4 yj = ye[j];
+            const double dx = yi[q].x - yj.x, dy = yi[q].y - yj.y, dz = yi[q].z - yj.z;
+            const double f = rbf_phi<KERN>(sqrt_spd((dx * dx + dy * dy) + dz * dz));
+            ss[row * H + ((dd - 1) ^ (row & (H - 1)))] = row < k && j < k ? f : 0.0;
         }
     }
     rbf_wave_sync();  // the partner rows' entries are read next
@@ -885,6 +942,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         }
         if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // bounded reads in flight
     }
+    if constexpr (PFR) stage2(li);  // the next quad's particle records
 
     // ---- 3. elimination without pivoting; pivot row c = lane c % 16, row set c / 16.
     //      Row set q is finished once c >= 16 q + 15 (all its rows are above the pivot): its
@@ -914,21 +972,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         rd[pq] = li == (c & 15) ? rp : rd[pq];
         // multipliers: a row set wholly below the pivot needs no test, a finished one none at all
         // (a zero pivot leaves garbage multipliers: the call then fails with PTV_E_SINGULAR)
+        // negated multipliers: A += u (-l) is one v_fmac_f64_dpp with the pivot row's u broadcast
+        // inside it (fma(-l, u, a) and fma(u, -l, a) round alike: bit-identical to k_rbf_spd)
         double l[R];
 #pragma unroll
         for (int q = 0; q < R; ++q) {
             const int row = li + 16 * q;
             if (16 * q + 15 <= c) l[q] = 0.0;
-            else if (16 * q > c) l[q] = A[q][c] * rp;
-            else l[q] = row > c ? A[q][c] * rp : 0.0;
+            else if (16 * q > c) l[q] = -(A[q][c] * rp);
+            else l[q] = row > c ? -(A[q][c] * rp) : 0.0;
         }
         double pivn = 0.0, rpn = 1.0;
 #pragma unroll
         for (int j = c + 1; j < M; ++j) {
-            const double u = PTV_BC(A[pq][j]);
-#pragma unroll
-            for (int q = 0; q < R; ++q)
-                if (16 * q + 15 > c) A[q][j] = fma(-l[q], u, A[q][j]);
+            if (R == 2 && pq == 0) fmac_bc_piv_n(c, A[R - 1][j], A[0][j], l[R - 1], l[0]);
+            else fmac_bc_self_n(c, A[pq][j], l[pq]);
             if (j == c + 1) {
                 pivn = rowbcast_n(c + 1, A[(c + 1) / 16][c + 1]);
                 rpn = rcp_nr(pivn);
@@ -936,10 +994,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         }
 #pragma unroll
         for (int t = 0; t < 3; ++t) {
-            const double u = PTV_BC(B[pq][t]);
-#pragma unroll
-            for (int q = 0; q < R; ++q)
-                if (16 * q + 15 > c) B[q][t] = fma(-l[q], u, B[q][t]);
+            if (R == 2 && pq == 0) fmac_bc_piv_n(c, B[R - 1][t], B[0][t], l[R - 1], l[0]);
+            else fmac_bc_self_n(c, B[pq][t], l[pq]);
         }
         piv = pivn;
         rp = rpn;
@@ -961,15 +1017,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 #pragma unroll
     for (int c = M - 1; c >= 0; --c) {
         const int pq = c / 16;
+        double u[R];  // this lane's U entries of column c (rows above c), the rest 0
+#pragma unroll
+        for (int q = 0; q < R; ++q) u[q] = li + 16 * q < c ? A[q][c] : 0.0;
 #pragma unroll
         for (int t = 0; t < 3; ++t) {
-            const double xc = PTV_BC(B[pq][t] * rd[pq]);
-#pragma unroll
-            for (int q = 0; q < R; ++q) {
-                if (16 * q < c) {  // row set q has rows above c
-                    const double u = li + 16 * q < c ? A[q][c] : 0.0;
-                    B[q][t] = fma(-u, xc, B[q][t]);
-                }
+            // B -= u x_c as B += (-x_c) u, the solution broadcast inside the fmac (same rounding)
+            const double nx = -(B[pq][t] * rd[pq]);
+            if (R == 2 && c > 16) {  // both row sets have rows above c (at c = 16 only set 0)
+                double bb[2] = {B[0][t], B[R - 1][t]};
+                const double uu[2] = {u[0], u[R - 1]};
+                fmac_bc_n<2>(c, bb, nx, uu);
+                B[0][t] = bb[0];
+                B[R - 1][t] = bb[1];
+            } else {
+                double bb[1] = {B[0][t]};
+                const double uu[1] = {u[0]};
+                fmac_bc_n<1>(c, bb, nx, uu);
+                B[0][t] = bb[0];
             }
         }
     }
@@ -980,24 +1045,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 #undef PTV_BC
 
     // ---- 5. evaluate at the voxel: sum_j phi(eps |x - y_j|) c_j ----
-    double qx, qy, qz;
-    if (a.separable) {
-        qx = ax[ix];
-        qy = ay[iy];
-        qz = az[iz];
-    } else {
-        qx = qpx[vfull];
-        qy = qpy[vfull];
-        qz = qpz[vfull];
-    }
     double o0 = 0.0, o1 = 0.0, o2 = 0.0;
 #pragma unroll
-    for (int q = 0; q < R; ++q) {
-        double e = 0.0;
-        if (li + 16 * q < k) {
-            const double dx = qx * eps - yi[q].x, dy = qy * eps - yi[q].y, dz = qz * eps - yi[q].z;
-            e = rbf_phi<KERN>(sqrt((dx * dx + dy * dy) + dz * dz));
-        }
+    for (int q = 0; q < R; ++q) {  // branch-free (rows past k: yi = 0, dropped)
+        const double dx = qx * eps - yi[q].x, dy = qy * eps - yi[q].y, dz = qz * eps - yi[q].z;
+        const double f = rbf_phi<KERN>(sqrt((dx * dx + dy * dy) + dz * dz));
+        const double e = li + 16 * q < k ? f : 0.0;
         o0 += e * B[q][0];
         o1 += e * B[q][1];
         o2 += e * B[q][2];
@@ -1005,28 +1058,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     o0 = seg_sum<16>(o0);
     o1 = seg_sum<16>(o1);
     o2 = seg_sum<16>(o2);
-    if (!valid || li != 0) return;
-    const size_t vo = (size_t)(iz - a.out_z0) * plane + rem;
-    if (!active) {
-        U[vo] = 0.0;
-        V[vo] = 0.0;
-        W[vo] = 0.0;
-        return;
+    if (valid && li == 0) {
+        if (active) {
+            if (singular) {
+                atomicAdd(&status[0], 1);
+                atomicMin(&status[1], (int)min((long long)vfull, 0x7fffffffLL));
+            }
+            if (slow) atomicOr(&status[2], 1);  // the host reruns this launch with k_rbf_spd
+            if (a.flags & PTV_FLAG_NAN_TO_NUM) {
+                auto fix = [](double x) { return x != x ? 0.0 : (x == INFINITY ? DBL_MAX : (x == -INFINITY ? -DBL_MAX : x)); };
+                o0 = fix(o0);
+                o1 = fix(o1);
+                o2 = fix(o2);
+            }
+        }
+        pend = true;
+        pvo = (size_t)(iz - a.out_z0) * plane + rem;
+        po[0] = active ? o0 : 0.0;
+        po[1] = active ? o1 : 0.0;
+        po[2] = active ? o2 : 0.0;
     }
-    if (singular) {
-        atomicAdd(&status[0], 1);
-        atomicMin(&status[1], (int)min((long long)vfull, 0x7fffffffLL));
-    }
-    if (slow) atomicOr(&status[2], 1);  // the host reruns this launch with k_rbf_spd
-    if (a.flags & PTV_FLAG_NAN_TO_NUM) {
-        auto fix = [](double x) { return x != x ? 0.0 : (x == INFINITY ? DBL_MAX : (x == -INFINITY ? -DBL_MAX : x)); };
-        o0 = fix(o0);
-        o1 = fix(o1);
-        o2 = fix(o2);
-    }
-    U[vo] = o0;
-    V[vo] = o1;
-    W[vo] = o2;
+    rbf_wave_sync();  // the next quad reuses this wave's LDS
+    }  // quads
+    flush();
 }
 
 template <int M, int KERN>
@@ -1156,9 +1210,12 @@ int launch_rbf(const RbfKernelArgs &ka, const Binned &b, const uint32_t *slots, 
     if (rbf_spd(ka, smooth)) {
         const char *e = dev_knob("PTV_RBF_SPD");  // dev knob: 1 = the LDS-broadcast SPD kernel
         if (!(e && e[0] == '1') && !ka.spd_lds && !(ka.flags & PTV_FLAG_RBF_SPD_LDS)) {
-            const long long waves = (nvox + 3) / 4;
-            const dim3 grid((unsigned)((waves + 3) / 4));
-#define PTV_S16(MM, KK) hipLaunchKernelGGL((k_rbf_spd16<MM, KK>), grid, dim3(256), 0, s, ka, b.prec, b.pval, slots, ax, ay, az, qx, qy, qz, mask, U, V, W, status)
+#define PTV_S16(MM, KK)                                                                                 \
+    do {                                                                                                \
+        static int occ = 0;                                                                             \
+        hipLaunchKernelGGL((k_rbf_spd16<MM, KK>), dim3(persistent_grid(k_rbf_spd16<MM, KK>, (nvox + 3) / 4, occ)), \
+                           dim3(256), 0, s, ka, b.prec, b.pval, slots, ax, ay, az, qx, qy, qz, mask, U, V, W, status); \
+    } while (0)
 #define PTV_S16K(MM) \
     switch (ka.kernel) { \
         case PTV_RBF_INVERSE_MULTIQUADRIC: PTV_S16(MM, PTV_RBF_INVERSE_MULTIQUADRIC); break; \

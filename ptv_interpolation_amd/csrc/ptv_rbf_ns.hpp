@@ -81,72 +81,6 @@ __device__ __forceinline__ void ns_prow(double (&row)[NP], const double4 &h, boo
 
 
 
-// ---- v_fmac_f64 with its first operand broadcast from lane N of the 16-lane row (gfx950 DPALU
-// DPP: row_newbcast only): acc += src[lane N] * mul in ONE instruction where the compiler emits a
-// v_mov_b64_dpp and a v_fma_f64 (it does not fold 64-bit DPP into the fmac).  Inline asm, so the
-// compiler cannot see the DPP read: each block starts with the s_nop 1 (2 wait states) a DPP read
-// needs after a VALU write of its source.  A block updates the accumulators of every live row set
-// of the lane (RS = 1 or 2) with one broadcast source. ----
-template <int N, int RS>
-__device__ __forceinline__ void fmac_bc(double (&acc)[RS], double src, const double (&mul)[RS]) {
-    if constexpr (RS == 1) {
-        asm("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
-            : "+v"(acc[0]) : "v"(src), "v"(mul[0]), "n"(N));
-    } else {
-        asm("s_nop 1\n\tv_fmac_f64_dpp %0, %2, %3 row_newbcast:%5 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-            "v_fmac_f64_dpp %1, %2, %4 row_newbcast:%5 row_mask:0xf bank_mask:0xf bound_ctrl:1"
-            : "+v"(acc[0]), "+v"(acc[1]) : "v"(src), "v"(mul[0]), "v"(mul[1]), "n"(N));
-    }
-}
-// the same where the source is the accumulator `piv` itself (the pivot row's set): the other set
-// `oth` first, then piv (its DPP read precedes its write)
-template <int N>
-__device__ __forceinline__ void fmac_bc_piv(double &oth, double &piv, double m_oth, double m_piv) {
-    asm("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-        "v_fmac_f64_dpp %1, %1, %3 row_newbcast:%4 row_mask:0xf bank_mask:0xf bound_ctrl:1"
-        : "+v"(oth), "+v"(piv) : "v"(m_oth), "v"(m_piv), "n"(N));
-}
-template <int N>
-__device__ __forceinline__ void fmac_bc_self(double &piv, double m_piv) {
-    asm("s_nop 1\n\tv_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf bound_ctrl:1"
-        : "+v"(piv) : "v"(m_piv), "n"(N));
-}
-#define PTV_NS_SW16(n, CALL)      \
-    switch ((n) & 15) {           \
-        case 0: CALL(0); break;   \
-        case 1: CALL(1); break;   \
-        case 2: CALL(2); break;   \
-        case 3: CALL(3); break;   \
-        case 4: CALL(4); break;   \
-        case 5: CALL(5); break;   \
-        case 6: CALL(6); break;   \
-        case 7: CALL(7); break;   \
-        case 8: CALL(8); break;   \
-        case 9: CALL(9); break;   \
-        case 10: CALL(10); break; \
-        case 11: CALL(11); break; \
-        case 12: CALL(12); break; \
-        case 13: CALL(13); break; \
-        case 14: CALL(14); break; \
-        default: CALL(15); break; \
-    }
-template <int RS>
-__device__ __forceinline__ void fmac_bc_n(int n, double (&acc)[RS], double src, const double (&mul)[RS]) {
-#define PTV_C(N) fmac_bc<N, RS>(acc, src, mul)
-    PTV_NS_SW16(n, PTV_C)
-#undef PTV_C
-}
-__device__ __forceinline__ void fmac_bc_piv_n(int n, double &oth, double &piv, double m_oth, double m_piv) {
-#define PTV_C(N) fmac_bc_piv<N>(oth, piv, m_oth, m_piv)
-    PTV_NS_SW16(n, PTV_C)
-#undef PTV_C
-}
-__device__ __forceinline__ void fmac_bc_self_n(int n, double &piv, double m_piv) {
-#define PTV_C(N) fmac_bc_self<N>(piv, m_piv)
-    PTV_NS_SW16(n, PTV_C)
-#undef PTV_C
-}
-
 #ifndef PTV_NS_STAMP
 #define PTV_NS_STAMP 0  // dev builds: per-wave s_memtime phase cycles into RbfKernelArgs::stamps
 #endif
@@ -261,7 +195,6 @@ __device__ __forceinline__ NsRec ns_rec(const double4 *__restrict__ prec, const 
     const double *q = reinterpret_cast<const double *>(pval + sl);
     return NsRec{p.x, p.y, p.z, p.w, q[0], q[1], q[2]};
 }
-__device__ uint8_t kNsMaskOn = 1;  // the mask byte read when there is no mask (global, not flat)
 
 template <int NC, int NP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_rbf_ns(
@@ -805,22 +738,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     rbf_wave_sync();  // the next quad reuses this wave's LDS
     }  // quads
     flush();
-}
-
-// persistent grid: the blocks one wave of residency holds (occupancy x CUs), a multiple of the 8
-// XCDs; a block that waited for a free CU would find its quads' share undone at the end
-inline unsigned ns_grid(long long nquad, int per_cu) {
-    static int cus[64];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-    int c = __atomic_load_n(&cus[dev], __ATOMIC_RELAXED);
-    if (c <= 0) {
-        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
-        __atomic_store_n(&cus[dev], c, __ATOMIC_RELAXED);
-    }
-    long long nb = (nquad + 3) / 4, cap = (long long)c * (per_cu > 0 ? per_cu : 1);
-    if (nb > cap) nb = cap;
-    return (unsigned)((nb + 7) / 8 * 8);
 }
 
 template <int NC, int NP>
