@@ -638,7 +638,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PTV_RBF_SPD
         if (krow && j < k) {
             const double4 yj = ye[j];
             const double dx = yi.x - yj.x, dy = yi.y - yj.y, dz = yi.z - yj.z;
-            e = rbf_phi<KERN>(sqrt((dx * dx + dy * dy) + dz * dz));
+            e = rbf_phi_d2<KERN>((dx * dx + dy * dy) + dz * dz);
         }
         sc[(dd - 1) * 64 + lane] = e;
     }
@@ -721,7 +721,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PTV_RBF_SPD
     double e = 0.0;
     if (krow) {
         const double dx = qx * eps - yi.x, dy = qy * eps - yi.y, dz = qz * eps - yi.z;
-        e = rbf_phi<KERN>(sqrt((dx * dx + dy * dy) + dz * dz));
+        e = rbf_phi_d2<KERN>((dx * dx + dy * dy) + dz * dz);
     }
     double o0 = seg_sum<L>(e * x0), o1 = seg_sum<L>(e * x1), o2 = seg_sum<L>(e * x2);
     if (!valid || li != 0) return;
@@ -917,7 +917,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
             const int j = (row + dd) & (NR - 1);
             const double4 yj = ye[j];
             const double dx = yi[q].x - yj.x, dy = yi[q].y - yj.y, dz = yi[q].z - yj.z;
-            const double f = rbf_phi<KERN>(sqrt_spd((dx * dx + dy * dy) + dz * dz));
+            const double f = rbf_phi_d2<KERN>((dx * dx + dy * dy) + dz * dz);
             ss[row * H + ((dd - 1) ^ (row & (H - 1)))] = row < k && j < k ? f : 0.0;
         }
     }
@@ -1049,7 +1049,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 #pragma unroll
     for (int q = 0; q < R; ++q) {  // branch-free (rows past k: yi = 0, dropped)
         const double dx = qx * eps - yi[q].x, dy = qy * eps - yi[q].y, dz = qz * eps - yi[q].z;
-        const double f = rbf_phi<KERN>(sqrt((dx * dx + dy * dy) + dz * dz));
+        const double f = rbf_phi_d2<KERN>((dx * dx + dy * dy) + dz * dz);
         const double e = li + 16 * q < k ? f : 0.0;
         o0 += e * B[q][0];
         o1 += e * B[q][1];

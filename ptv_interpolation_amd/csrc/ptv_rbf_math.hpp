@@ -106,6 +106,17 @@ __device__ __forceinline__ double rbf_phi(double r) {
     return 0.0;
 }
 
+// the SPD kernels from the squared distance (r * r -> d2: no square root for the Gaussian and the
+// inverse quadratic; within an ulp of scipy's r**2, far inside the solve's conditioning)
+template <int KERN>
+__device__ __forceinline__ double rbf_phi_d2(double d2) {
+    static_assert(KERN == PTV_RBF_GAUSSIAN || KERN == PTV_RBF_INVERSE_QUADRATIC || KERN == PTV_RBF_INVERSE_MULTIQUADRIC,
+                  "SPD kernels");
+    if constexpr (KERN == PTV_RBF_INVERSE_MULTIQUADRIC) return 1.0 / sqrt(d2 + 1.0);
+    if constexpr (KERN == PTV_RBF_INVERSE_QUADRATIC) return 1.0 / (d2 + 1.0);
+    return exp_nonpos(-d2);
+}
+
 static __device__ double rbf_phi_rt(int kern, double r) {
     switch (kern) {
         case PTV_RBF_LINEAR: return rbf_phi<PTV_RBF_LINEAR>(r);
