@@ -384,3 +384,28 @@ def test_nullspace_list_overflow_reruns_with_pivoting(ctx):
     for a, b in zip((U, V, W), ref):
         assert np.isfinite(a).all()
         assert normwise(a, b) <= TOL
+
+
+@pytest.mark.parametrize("shape", [(1, 1, 1), (1, 1, 3), (2, 3, 5), (1, 7, 1)])
+@pytest.mark.parametrize("kernel,k,eps,degree", [
+    ("thin_plate_spline", 20, None, None),  # k_rbf_ns<20, 4>
+    ("gaussian", 32, 1.5, -1),              # k_rbf_spd16<32>
+])
+def test_persistent_kernels_on_tiny_grids(ctx, shape, kernel, k, eps, degree):
+    """The persistent null-space and SPD kernels take quads (4 voxels) from per-XCD ranges of an
+    occupancy-sized grid: grids of fewer voxels than one quad, one block or one XCD's share (most
+    waves and whole XCDs idle, a partial last quad) match the oracle."""
+    from oracle import cpu_ref
+    from ptv_interpolation_amd.rbf import LocalRBFInterpolator
+
+    rng = np.random.default_rng(sum(shape) * 7 + k)
+    P = rng.uniform(0, 6, (400, 3))
+    Q = rng.standard_normal((400, 3))
+    nz, ny, nx = shape
+    ax, ay, az = (np.linspace(1.0, 5.0, n) for n in (nx, ny, nz))
+    it = LocalRBFInterpolator(P, Q, neighbors=k, kernel=kernel, epsilon=eps, degree=degree)
+    got = it.evaluate_grid(ax, ay, az)
+    ref = cpu_ref.rbf_local_grid(P, Q, ax, ay, az, k, kernel, eps, degree)
+    for a, b in zip(got, ref):
+        assert a.shape == (nz, ny, nx)
+        assert normwise(a, b) <= TOL_ILL if kernel == "gaussian" else normwise(a, b) <= TOL
