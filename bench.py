@@ -17,8 +17,10 @@ was given equals ``--gpus`` and fails loudly otherwise.
 
 Multi-GPU = the north_star partition (zslab.py): ONE grid cut into z-slabs,
 rank r computing planes slab_bounds(nz, N)[r], the particle set replicated in every rank's HBM
-(broadcast before the timed loop) and culled on device to the slab's window with a proof of
-exactness (ptv_knn_params.slab_halo; a failed proof widens the halo, never changes a result).
+(broadcast before the timed loop) and culled on device by a per-column map derived from the
+slab's own lattice bounds, proven exact on the device before every main launch
+(PTV_FLAG_SLAB_CULL_AUTO; the warmup's first call builds the map; a failed proof reruns the call
+unculled, never changes a result).
 No collective touches the timed step; an RCCL all-gather reassembly of the full field (slabs
 padded to the largest one when they differ) is timed once after it and reported apart
 (``allgather_ms``).
@@ -168,7 +170,9 @@ def parse():
                          "are skipped and written as 0")
     ap.add_argument("--div", action="store_true", default=None,
                     help="k-NN methods: + consistent divergence of each slab (C5)")
-    ap.add_argument("--halo", type=float, default=None, help="N>1: first slab_halo to try (default: 4 k-NN radii)")
+    ap.add_argument("--halo", type=float, default=None,
+                    help="N>1: the scalar slab_halo cull starting at this halo (zslab.interp_slab retries) instead "
+                         "of the per-column map (PTV_FLAG_SLAB_CULL_AUTO, default)")
     ap.add_argument("--r0-scale", type=float, default=0.0, help="dev: first search radius / expected k-NN radius")
     ap.add_argument("--cpu-sample-planes", type=int, default=None)
     ap.add_argument("--cpu-workers", type=int, default=None)
@@ -611,8 +615,7 @@ def main_interp(args):
     if radius:
         method = _lib.METHOD_IDW_RADIUS
     cull = world > 1 and not rbf and not radius
-    halo = zslab.HaloState(args.halo if args.halo is not None else
-                           zslab.halo_guess(n, (G, G, nz), k))
+    halo = zslab.HaloState(args.halo) if (cull and args.halo is not None) else None
     ptrs = [c.data_ptr() for c in cols]
     aptrs = [a.data_ptr() for a in axes]
     optrs = [o.data_ptr() for o in out]
@@ -624,7 +627,8 @@ def main_interp(args):
             ctx.interp_rbf_dev(n, ptrs, G, G, nz, axes_ptrs=aptrs, out_ptrs=optrs, k=k, kernel=kern, epsilon=eps,
                                degree=deg, z_range=(za, zb), stream=stream)
             return
-        flags = (_lib.FLAG_OUT_F32 if out_f32 else 0) | (_lib.FLAG_NAN_TO_NUM if args.mask else 0)
+        flags = ((_lib.FLAG_OUT_F32 if out_f32 else 0) | (_lib.FLAG_NAN_TO_NUM if args.mask else 0) |
+                 (_lib.FLAG_SLAB_CULL_AUTO if cull and halo is None else 0))
         mptr = mask_t.data_ptr() if (mask_t is not None and args.mask) else 0
 
         def call(h):
@@ -632,7 +636,7 @@ def main_interp(args):
                                       power=args.power, stream=stream, mask_ptr=mptr, r0_scale=args.r0_scale,
                                       flags=flags, z_range=(za, zb), slab_halo=h, radius=radius)
 
-        zslab.interp_slab(call, halo) if cull else call(0.0)
+        zslab.interp_slab(call, halo) if halo is not None else call(0.0)
         if args.div:
             dtc = _lib.F32 if out_f32 else _lib.F64
             ctx.divergence_dev(G, G, zb - za, [o.data_ptr() for o in out], mask_t[za:zb].data_ptr(),
@@ -645,7 +649,8 @@ def main_interp(args):
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    rec = {key: [] for key in ("ms_knn", "ms_lattice", "ms_bin", "ms_solve", "ms_cull", "ms_stencil", "n_binned")}
+    rec = {key: [] for key in ("ms_knn", "ms_lattice", "ms_bin", "ms_solve", "ms_cull", "ms_stencil", "n_binned",
+                               "n_rbf_pivoted")}
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -702,7 +707,9 @@ def main_interp(args):
                 "frac": round(tf / FP64_PEAK_TFLOPS, 4), "traffic": None,
                 "kernel": rbf_kernel_label(kern, k, m_sys, deg),
                 "alg_flops_per_launch": flops, "kernel_ms": round(avg["ms_solve"], 3),
-                "knn_slots_ms": round(avg["ms_knn"], 3)}
+                "knn_slots_ms": round(avg["ms_knn"], 3),
+                # voxels the null-space kernel handed to the pivoting kernel per step (max over steps)
+                "n_rbf_pivoted": int(max(rec["n_rbf_pivoted"])) if rec["n_rbf_pivoted"] else 0}
     else:
         Vk = (zb - za) * G * G  # voxels the k-NN launch computes (slab + redundant halo planes)
         if radius:  # gather model with the measured mean ball population in place of k
@@ -773,7 +780,7 @@ def main_interp(args):
                        "particles_replicated": n, "method": args.method, "k": k, "power": args.power,
                        "out_dtype": "f32" if out_f32 else "f64", "mask": bool(args.mask), "div": bool(args.div),
                        "planes": [z0, z1],
-                       "parallelism": f"z-slab x{world}" + (" (particles replicated, slab_halo cull)" if cull else "")},
+                       "parallelism": f"z-slab x{world}" + (" (particles replicated, per-slab cull)" if cull else "")},
             "roofline": roof,
             "cpu_baseline": cpu,
             "breakdown_ms": {"bin": round(avg["ms_bin"], 3), "cull": round(avg["ms_cull"], 3),
@@ -785,7 +792,9 @@ def main_interp(args):
         if args.mask:
             line["fluid_mvoxels_per_s"] = round(value * fluid_frac, 2)
         if cull:
-            line["halo"] = {**halo.as_dict(), "particles_binned": int(avg["n_binned"])}
+            line["cull"] = ({"mode": "scalar slab_halo", **halo.as_dict()} if halo is not None else
+                            {"mode": "per-column map (PTV_FLAG_SLAB_CULL_AUTO), proven on the device"})
+            line["cull"]["particles_binned"] = int(avg["n_binned"])
         if gather_ms is not None:
             line["allgather_ms"] = round(gather_ms, 2) if isinstance(gather_ms, float) else gather_ms
         if e2e is not None:

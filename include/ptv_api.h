@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define PTV_API_VERSION 9
+#define PTV_API_VERSION 10
 
 /* error codes */
 #define PTV_OK 0
@@ -70,6 +70,20 @@ extern "C" {
 /* k-NN, diagnostics (k >= 13): near-tie repair list of one entry, so that a launch with two or more
  * tiles to repair takes the whole-launch exact rerun (the path past the 2^22-tile list) (ABI v9) */
 #define PTV_FLAG_KNN_REPAIR_ALL 16u
+/* k-NN interpolation on a z-slab of a separable grid (z_begin > 0 or z_end < nz): bin only the
+ * particles that can be among a slab voxel's k nearest, by a per-(x, y)-column cull map (ABI v10).
+ * Replaces the scalar slab_halo (ignored under this flag) for the multi-GPU z-slab split with the
+ * particle set replicated (interpolator.py:173-182 fanned out over GPUs).  The
+ * context derives the map from the slab's own finest lattice bounds: every voxel v of a lattice
+ * cell Q has d_k(v) <= U(Q) = max over Q's corners of D(c) + Q's half diagonal, so only particles
+ * within U(Q) of some cell Q are needed; per column that is a height above / depth below the slab.
+ * The first call for a (particle arrays, n, 96-value fingerprint, grid, slab, k, method) key bins
+ * every particle and caches the map; later calls cull with it and PROVE on the device, from the
+ * lattice of the kept particles, that the map covers what the slab needs before the main kernel
+ * runs (a failed proof -- the particles changed under the same arrays -- reruns the call without
+ * the cull and refreshes the map).  Results are bit-identical to the unculled call.
+ * ptv_stats.n_binned reports the particles kept. */
+#define PTV_FLAG_SLAB_CULL_AUTO 32u
 
 typedef struct ptv_ctx ptv_ctx;
 

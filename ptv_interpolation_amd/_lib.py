@@ -86,6 +86,7 @@ FLAG_OUT_F32 = 2  # U, V, W written as float32 (main.py:230 astype, fused)
 FLAG_RBF_SPD_LDS = 4  # local RBF diagnostics: SPD systems through the LDS-broadcast kernel
 FLAG_RBF_PIVOTING = 8  # local RBF diagnostics: scale-invariant kernels through the pivoting solver
 FLAG_KNN_REPAIR_ALL = 16  # k-NN diagnostics: near-tie repair reruns the whole launch past one tile
+FLAG_SLAB_CULL_AUTO = 32  # k-NN z-slab calls: per-column cull map, cached per context and proven (ABI v10)
 
 
 class DivParams(C.Structure):

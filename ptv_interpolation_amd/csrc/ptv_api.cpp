@@ -74,6 +74,14 @@ struct ptv_ctx {
     DevBuf<double> lat_axes[kMaxLattice], lat_dk[kMaxLattice];  // coarse-lattice bound levels
     DevBuf<float4> lat_recs[kMaxLattice];                        // their k-NN records (seeds, fp32 relative)
     DevBuf<int> lat_order[kMaxLattice];                          // longest-first block order per level
+    DevBuf<uint32_t> lat_split;                                  // split lattice launch: partial lists
+    // PTV_FLAG_SLAB_CULL_AUTO: the cached per-column cull map (top, bot), its key, the proof's
+    // need map and scratch
+    DevBuf<double> cmap[2], cneed[2], ccols, cfp;
+    DevBuf<unsigned long long> ckeys;
+    CullMap cmap_geo{};
+    bool cmap_valid = false;
+    std::vector<double> ckey, ckey_new;
     DevBuf<uint32_t> slots;                                      // local RBF: chunk k-NN slots
     DevBuf<int> rbf_pw, rbf_status;                              // monomial exponents, singular count
     DevBuf<uint32_t> rbf_nslist;                                 // local RBF: voxels k_rbf_ns hands over
@@ -219,6 +227,12 @@ int ptv_free(ptv_ctx *c) {
     for (auto &b : c->lat_dk) b.release();
     for (auto &b : c->lat_recs) b.release();
     for (auto &b : c->lat_order) b.release();
+    c->lat_split.release();
+    for (auto &b : c->cmap) b.release();
+    for (auto &b : c->cneed) b.release();
+    c->ccols.release();
+    c->cfp.release();
+    c->ckeys.release();
     c->slots.release();
     c->rbf_pw.release();
     c->rbf_status.release();
@@ -292,6 +306,11 @@ constexpr double kDefaultR0Scale = 1.0;     // first gather radius / expected k-
 constexpr long long kMaxCells = 1LL << 28;
 constexpr long long kLatticeStopPoints = 50000; // no coarser lattice below this many points
 constexpr size_t kSeedBytesMax = 40ULL << 30;    // lattice seed records per level (C5 2048^3, k = 8: 17 GB)
+// split lattice launch (k_kdist_merge): the first max(kLatticeSplitMinBlocks, blocks /
+// kLatticeSplitDiv) blocks of a lattice level's longest-first order, kLatticeSplit waves per tile
+constexpr int kLatticeSplit = 16;
+constexpr long long kLatticeSplitMinBlocks = 8;
+constexpr long long kLatticeSplitDiv = 128;
 
 int validate(const ptv_particles *p, const ptv_grid *g, const void *prm) {
     if (!p || !g || !prm) {
@@ -571,6 +590,17 @@ int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchP
             PTV_TRY(launch_block_order(lat[l + 1].dk, lat[l + 1].n, lat[l].n[0], lat[l].n[1], lat[l].n[2], kl.r0,
                                        c->lat_order[l].p, s));
             ll.order = c->lat_order[l].p;
+            // the first blocks of the order (the void tiles) as a split launch (k_kdist_merge)
+            int split = kLatticeSplit;
+            long long sblk = std::min<long long>(nb, std::max<long long>(kLatticeSplitMinBlocks, nb / kLatticeSplitDiv));
+            if (const char *e = dev_knob("PTV_LAT_SPLIT")) split = std::atoi(e);          // dev: 0 = off
+            if (const char *e = dev_knob("PTV_LAT_SPLIT_BLOCKS")) sblk = std::min<long long>(nb, std::atoll(e));
+            if (split > 1 && sblk > 0) {
+                PTV_TRY(c->lat_split.ensure(kdist_split_slots(split, (int)sblk, kmax_for(prm->k))));
+                ll.split = split;
+                ll.split_blocks = (int)sblk;
+                ll.split_out = c->lat_split.p;
+            }
         }
         ll.kd_recs = lat[l].recs;
         ll.nx = lat[l].n[0];
@@ -648,9 +678,166 @@ SearchParams knn_search(const ptv_knn_params *prm) {
                         prm->lattice_bounds};
 }
 
+// PTV_FLAG_SLAB_CULL_AUTO (see ptv_api.h): the per-column cull map, cached per context.  A call
+// whose key matches the cached map culls with it and proves the cull on the device (the need map
+// of the kept particles' lattice inside the used map everywhere) before the gated main launch; a
+// call without a cached map (or whose proof fails) bins every particle and builds the map from its
+// own lattice.  Key: the particle arrays, n, a 96-value fingerprint, the grid, the slab, k, method.
+int run_knn_auto(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn_params *prm,
+                 const double *ax, const double *ay, const double *az, const uint8_t *mask, double *U, double *V,
+                 double *W, hipStream_t s, ptv_stats *st) {
+    const SearchParams sp = knn_search(prm);
+    const int64_t n = p->n;
+    const double *src[6] = {p->x, p->y, p->z, p->u, p->v, p->w};
+    PTV_TRY(c->cfp.ensure(6 * kFingerprint));
+    PTV_TRY(launch_fingerprint(src, n, c->cfp.p, s));
+    std::vector<double> &key = c->ckey_new;
+    key.assign(6 * kFingerprint, 0.0);
+    PTV_HIP(hipMemcpyAsync(key.data(), c->cfp.p, 6 * kFingerprint * sizeof(double), hipMemcpyDeviceToHost, s));
+    PTV_HIP(hipStreamSynchronize(s));
+    for (const void *q : {(const void *)p->x, (const void *)p->y, (const void *)p->z, (const void *)p->u,
+                          (const void *)p->v, (const void *)p->w, (const void *)ax, (const void *)ay,
+                          (const void *)az}) {
+        uint64_t bits = (uint64_t)(uintptr_t)q;
+        double d;
+        std::memcpy(&d, &bits, sizeof(d));
+        key.push_back(d);
+    }
+    for (int64_t v : {n, g->nx, g->ny, g->nz, g->z_begin, g->z_end, (int64_t)prm->k, (int64_t)prm->method,
+                      (int64_t)prm->lattice_bounds})
+        key.push_back((double)v);
+    // bitwise comparison (a NaN fingerprint value never matches itself otherwise)
+    bool use_map = c->cmap_valid && c->ckey.size() == key.size() &&
+                   std::memcmp(c->ckey.data(), key.data(), key.size() * sizeof(double)) == 0;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        KnnLaunch kl;
+        Binned b{};
+        ptv_particles pe = *p;
+        bool culled = false;
+        c->cull_timed = false;
+        if (use_map) {
+            const size_t nb = cull_blocks(n);
+            for (auto &d : c->cull) PTV_TRY(d.ensure(n));
+            PTV_TRY(c->cull_win.ensure(4));
+            PTV_TRY(c->cull_cnt.ensure(nb + 1));
+            double *dst[6];
+            for (int a = 0; a < 6; ++a) dst[a] = c->cull[a].p;
+            CullMap used = c->cmap_geo;
+            used.top = c->cmap[0].p;
+            used.bot = c->cmap[1].p;
+            uint32_t *h_total = reinterpret_cast<uint32_t *>(c->h_misc);
+            PTV_HIP(hipEventRecord(c->ev_cull0, s));
+            PTV_TRY(launch_cull(src, n, az, (int)g->z_begin, (int)g->z_end, 0.0, c->cull_win.p, c->cull_cnt.p, dst,
+                                nullptr, s, &used));
+            PTV_TRY(c->bbox_part.ensure(6 * 1024));
+            PTV_TRY(c->bbox_out.ensure(8));
+            const double *kp[3] = {dst[0], dst[1], dst[2]};
+            const double *qa[3] = {ax, ay, az + g->z_begin};
+            const int64_t qn[3] = {g->nx, g->ny, g->z_end - g->z_begin};
+            PTV_TRY(launch_bbox(kp, n, qa, qn, c->bbox_part.p, 1024, c->bbox_out.p, s, c->cull_cnt.p + nb));
+            PTV_HIP(hipMemcpyAsync(c->h_bbox, c->bbox_out.p, 6 * sizeof(double), hipMemcpyDeviceToHost, s));
+            PTV_HIP(hipMemcpyAsync(h_total, c->cull_cnt.p + nb, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+            PTV_HIP(hipEventRecord(c->ev_cull1, s));
+            PTV_HIP(hipStreamSynchronize(s));
+            const int64_t kept = (int64_t)*h_total;
+            if (kept >= prm->k) {
+                pe = ptv_particles{kept, dst[0], dst[1], dst[2], dst[3], dst[4], dst[5]};
+                culled = true;
+                c->cull_timed = true;
+            }
+        }
+        PTV_TRY(prepare(c, &pe, g, &sp, ax, ay, az, nullptr, nullptr, nullptr, s, kl, b, culled ? c->h_bbox : nullptr));
+        if (kl.cb.dk == nullptr) {
+            // no lattice bounds (nothing to prove the cull or to build a map from): every particle
+            if (culled) {
+                culled = false;
+                c->cull_timed = false;
+                PTV_TRY(prepare(c, p, g, &sp, ax, ay, az, nullptr, nullptr, nullptr, s, kl, b));
+            }
+            PTV_TRY(launch_knn(kl, b, ax, ay, az, nullptr, nullptr, nullptr, mask, U, V, W, s));
+            PTV_HIP(hipEventRecord(c->ev_knn1, s));
+            c->timed_pending = true;
+            if (st) *st = c->last;
+            return PTV_OK;
+        }
+        // the map geometry: cells of two finest-lattice cells per axis over the grid's (x, y) extent
+        // (edge cells reach to infinity, so any extent is valid; it only sets the resolution)
+        CullMap geo = c->cmap_geo;
+        if (!culled) {
+            double e[4];
+            PTV_HIP(hipMemcpyAsync(&e[0], ax, sizeof(double), hipMemcpyDefault, s));
+            PTV_HIP(hipMemcpyAsync(&e[1], ax + (g->nx - 1), sizeof(double), hipMemcpyDefault, s));
+            PTV_HIP(hipMemcpyAsync(&e[2], ay, sizeof(double), hipMemcpyDefault, s));
+            PTV_HIP(hipMemcpyAsync(&e[3], ay + (g->ny - 1), sizeof(double), hipMemcpyDefault, s));
+            PTV_HIP(hipStreamSynchronize(s));
+            geo = CullMap{};
+            geo.mx = std::max(1, std::min(256, (kl.cb.n[0] - 1) / 2));
+            geo.my = std::max(1, std::min(256, (kl.cb.n[1] - 1) / 2));
+            geo.x0 = std::min(e[0], e[1]);
+            geo.y0 = std::min(e[2], e[3]);
+            const double wx = std::fabs(e[1] - e[0]), wy = std::fabs(e[3] - e[2]);
+            geo.cw = wx > 0.0 && std::isfinite(wx) ? wx / geo.mx : 1.0;
+            geo.ch = wy > 0.0 && std::isfinite(wy) ? wy / geo.my : 1.0;
+            if (!std::isfinite(geo.x0)) geo.x0 = 0.0;
+            if (!std::isfinite(geo.y0)) geo.y0 = 0.0;
+            geo.icw = 1.0 / geo.cw;
+            geo.ich = 1.0 / geo.ch;
+        }
+        const size_t nm = (size_t)geo.mx * geo.my;
+        const size_t ncol = (size_t)std::max(kl.cb.n[0] - 1, 1) * std::max(kl.cb.n[1] - 1, 1);
+        PTV_TRY(c->ccols.ensure(7 * ncol));
+        PTV_TRY(c->ckeys.ensure(2 * nm));
+        PTV_TRY(c->halo_need.ensure(1));
+        if (culled) {
+            // the proof, gating the main launch: the kept particles' lattice needs no more than the map
+            for (auto &d : c->cneed) PTV_TRY(d.ensure(nm));
+            CullMap used = geo;
+            used.top = c->cmap[0].p;
+            used.bot = c->cmap[1].p;
+            PTV_TRY(launch_cull_need(kl.cb.ax, kl.cb.ay, kl.cb.az, kl.cb.n, kl.cb.dk, kl.cg.mg, geo, c->cneed[0].p,
+                                     c->cneed[1].p, c->ccols.p, c->ckeys.p, &used, c->halo_need.p, s));
+            kl.gate = c->halo_need.p;
+            kl.gate_halo = 0.0;
+            PTV_HIP(hipEventRecord(c->ev_main0, s));
+        }
+        PTV_TRY(launch_knn(kl, b, ax, ay, az, nullptr, nullptr, nullptr, mask, U, V, W, s));
+        PTV_HIP(hipEventRecord(c->ev_knn1, s));
+        c->timed_pending = true;
+        c->last.n_particles = n;
+        c->last.n_binned = pe.n;
+        if (!culled) {
+            // every particle binned: this call's lattice gives the map later calls cull with
+            for (auto &d : c->cmap) PTV_TRY(d.ensure(nm));
+            PTV_TRY(launch_cull_need(kl.cb.ax, kl.cb.ay, kl.cb.az, kl.cb.n, kl.cb.dk, kl.cg.mg, geo, c->cmap[0].p,
+                                     c->cmap[1].p, c->ccols.p, c->ckeys.p, nullptr, nullptr, s));
+            c->cmap_geo = geo;
+            c->cmap_valid = true;
+            c->ckey = key;
+            if (st) *st = c->last;
+            return PTV_OK;
+        }
+        PTV_HIP(hipMemcpyAsync(c->h_misc + 1, c->halo_need.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+        PTV_HIP(hipStreamSynchronize(s));
+        if (c->h_misc[1] == 0ull) {  // proven: the gated launch wrote every output
+            c->last.halo_required = 0.0;
+            if (st) *st = c->last;
+            return PTV_OK;
+        }
+        // not proven (the particles changed under the same arrays and fingerprint): no outputs were
+        // written; again with every particle binned, which refreshes the map
+        c->cmap_valid = false;
+        use_map = false;
+    }
+    set_error("slab cull map: unreachable retry state");
+    return PTV_E_HIP;
+}
+
 int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn_params *prm, const double *ax,
             const double *ay, const double *az, const double *qx, const double *qy, const double *qz,
             const uint8_t *mask, double *U, double *V, double *W, hipStream_t s, ptv_stats *st) {
+    if ((prm->flags & PTV_FLAG_SLAB_CULL_AUTO) && prm->method != PTV_METHOD_IDW_RADIUS && ax != nullptr &&
+        (g->z_begin > 0 || g->z_end < g->nz) && lattice_built(g, prm->lattice_bounds))
+        return run_knn_auto(c, p, g, prm, ax, ay, az, mask, U, V, W, s, st);
     SearchParams sp = knn_search(prm);
     const bool radius = prm->method == PTV_METHOD_IDW_RADIUS;
     if (radius) {

@@ -363,18 +363,31 @@ __global__ __launch_bounds__(256) void k_slab_window(const double *__restrict__ 
 
 __device__ __forceinline__ bool in_window(double z, const double *win) { return z >= win[0] && z <= win[1]; }
 
-__global__ __launch_bounds__(256) void k_cull_count(const double *__restrict__ z, int64_t n,
-                                                    const double *__restrict__ win, uint32_t *__restrict__ bcount) {
+// the cull test of particle i: z inside the window [win[0], win[1]], or (per-column map) above it
+// up to the top of its (x, y) cell / below it down to the bottom
+__device__ __forceinline__ bool cull_keep(const double *__restrict__ x, const double *__restrict__ y,
+                                          const double *__restrict__ z, int64_t i, double lo, double hi,
+                                          const CullMap &m) {
+    const double v = z[i];
+    if (v >= lo && v <= hi) return true;
+    if (m.top == nullptr) return false;
+    const int cx = (int)fmin(fmax(floor((x[i] - m.x0) * m.icw), 0.0), (double)(m.mx - 1));
+    const int cy = (int)fmin(fmax(floor((y[i] - m.y0) * m.ich), 0.0), (double)(m.my - 1));
+    const int c = cy * m.mx + cx;
+    return v > hi ? v <= m.top[c] : v >= m.bot[c];  // NaN coordinates: never kept
+}
+
+__global__ __launch_bounds__(256) void k_cull_count(const double *__restrict__ x, const double *__restrict__ y,
+                                                    const double *__restrict__ z, int64_t n,
+                                                    const double *__restrict__ win, CullMap m,
+                                                    uint32_t *__restrict__ bcount) {
     const double lo = win[0], hi = win[1];
     const int64_t base = (int64_t)blockIdx.x * kCullTile + threadIdx.x;
     uint32_t c = 0;
 #pragma unroll
     for (int j = 0; j < kCullItems; ++j) {
         const int64_t i = base + (int64_t)j * 256;
-        if (i < n) {
-            const double v = z[i];
-            c += (v >= lo && v <= hi) ? 1u : 0u;
-        }
+        if (i < n) c += cull_keep(x, y, z, i, lo, hi, m) ? 1u : 0u;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
@@ -391,7 +404,7 @@ struct Cols6 {
 
 // item (j, thread) of a block is particle base + j*256 + thread: j-major, thread-minor is
 // index order, so the ranks below preserve it
-__global__ __launch_bounds__(256) void k_cull_write(Cols6 c, int64_t n, const double *__restrict__ win,
+__global__ __launch_bounds__(256) void k_cull_write(Cols6 c, int64_t n, const double *__restrict__ win, CullMap m,
                                                     const uint32_t *__restrict__ boff) {
     const double lo = win[0], hi = win[1];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -402,10 +415,7 @@ __global__ __launch_bounds__(256) void k_cull_write(Cols6 c, int64_t n, const do
     for (int j = 0; j < kCullItems; ++j) {
         const int64_t i = base + (int64_t)j * 256;
         keep[j] = false;
-        if (i < n) {
-            const double v = c.src[2][i];
-            keep[j] = v >= lo && v <= hi;
-        }
+        if (i < n) keep[j] = cull_keep(c.src[0], c.src[1], c.src[2], i, lo, hi, m);
         const unsigned long long m = __builtin_amdgcn_ballot_w64(keep[j]);
         if (lane == 0) wcnt[j][wid] = (uint32_t)__builtin_popcountll(m);
     }
@@ -429,19 +439,187 @@ __global__ __launch_bounds__(256) void k_cull_write(Cols6 c, int64_t n, const do
 size_t cull_blocks(int64_t n) { return (size_t)((n + kCullTile - 1) / kCullTile); }
 
 int launch_cull(const double *const src[6], int64_t n, const double *az, int z0, int z1, double halo, double *win,
-                uint32_t *bcount, double *const dst[6], uint32_t *h_total, hipStream_t s) {
+                uint32_t *bcount, double *const dst[6], uint32_t *h_total, hipStream_t s, const CullMap *map) {
     const int nb = (int)cull_blocks(n);
-    hipLaunchKernelGGL(k_slab_window, dim3(1), dim3(256), 0, s, az, z0, z1, halo, win);
-    hipLaunchKernelGGL(k_cull_count, dim3(nb), dim3(256), 0, s, src[2], n, (const double *)win, bcount);
+    const CullMap m = map != nullptr ? *map : CullMap{};
+    hipLaunchKernelGGL(k_slab_window, dim3(1), dim3(256), 0, s, az, z0, z1, map != nullptr ? 0.0 : halo, win);
+    hipLaunchKernelGGL(k_cull_count, dim3(nb), dim3(256), 0, s, src[0], src[1], src[2], n, (const double *)win, m,
+                       bcount);
     hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(1024), 0, s, bcount, nb);  // total -> bcount[nb]
     Cols6 c;
     for (int a = 0; a < 6; ++a) {
         c.src[a] = src[a];
         c.dst[a] = dst[a];
     }
-    hipLaunchKernelGGL(k_cull_write, dim3(nb), dim3(256), 0, s, c, n, (const double *)win, (const uint32_t *)bcount);
+    hipLaunchKernelGGL(k_cull_write, dim3(nb), dim3(256), 0, s, c, n, (const double *)win, m, (const uint32_t *)bcount);
     PTV_HIP(hipGetLastError());
     if (h_total != nullptr) PTV_HIP(hipMemcpyAsync(h_total, bcount + nb, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    return PTV_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Per-column cull map (PTV_FLAG_SLAB_CULL_AUTO).  Every slab voxel v lies in a cell Q of the
+// slab's finest lattice, and with the cell's corner bounds D(c) (k-th distance of the lattice
+// point c, from the particles binned) d_k(v) <= D(c*) + |v - c*| for its nearest corner c*, so
+// d_k(v) <= U(Q) = max_c D(c) + diag(Q) / 2 over the whole cell.  A particle p that is among
+// v's k nearest therefore lies within U(Q) of the box Q.  Above the slab (z > Q's top z1) that
+// means z <= z1 + sqrt(U^2 - gap_xy(p, Q)^2): the map keeps, for each (x, y) cell, the largest
+// such height over every lattice cell that reaches it (and the lowest depth below the slab).
+// Per lattice column (i, j) the cells l are folded into T = max_l (z1 + U), B = min_l (z0 - U)
+// and Rm = max_l U; since r - sqrt(r^2 - g^2) decreases in r, T - Rm + sqrt(Rm^2 - g^2) bounds
+// every cell's height of the column (B + Rm - sqrt(...) every depth).  A culled particle is then
+// strictly farther than U(Q) from every cell, so it is neither among any voxel's k nearest nor
+// tied with the k-th.  Margins: relative 1e-9 on every distance plus the binning margin.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long ord_key(double v) {  // monotone double -> u64
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double ord_val(unsigned long long k) {
+    return __longlong_as_double((long long)((k >> 63) ? (k & 0x7fffffffffffffffull) : ~k));
+}
+
+constexpr int kColFields = 7;  // x lo, x hi, y lo, y hi, T, B, Rm
+
+__global__ __launch_bounds__(256) void k_cull_columns(const double *__restrict__ lax, const double *__restrict__ lay,
+                                                      const double *__restrict__ laz, int n0, int n1, int n2,
+                                                      const double *__restrict__ dk, double mg,
+                                                      double *__restrict__ cols) {
+    const int c0 = max(n0 - 1, 1), c1 = max(n1 - 1, 1), c2 = max(n2 - 1, 1);
+    const int t = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (t >= c0 * c1) return;
+    const int i = t % c0, j = t / c0;
+    const int i1 = min(i + 1, n0 - 1), j1 = min(j + 1, n1 - 1);
+    const double xa = lax[i], xb = lax[i1], ya = lay[j], yb = lay[j1];
+    const double dx = fabs(xb - xa), dy = fabs(yb - ya);
+    auto D = [&](int a, int b, int l) { return dk[((size_t)l * n1 + b) * n0 + a]; };
+    double T = -INFINITY, B = INFINITY, Rm = 0.0;
+    for (int l = 0; l < c2; ++l) {
+        const int l1 = min(l + 1, n2 - 1);
+        const double za = laz[l], zb = laz[l1];
+        const double dz = fabs(zb - za);
+        const double dmax = fmax(fmax(fmax(D(i, j, l), D(i1, j, l)), fmax(D(i, j1, l), D(i1, j1, l))),
+                                 fmax(fmax(D(i, j, l1), D(i1, j, l1)), fmax(D(i, j1, l1), D(i1, j1, l1))));
+        const double U = (dmax + 0.5 * sqrt((dx * dx + dy * dy) + dz * dz)) * (1.0 + 1e-9) + mg;
+        T = fmax(T, fmax(za, zb) + U);
+        B = fmin(B, fmin(za, zb) - U);
+        Rm = fmax(Rm, U);
+    }
+    if (!(Rm < INFINITY)) Rm = INFINITY;  // NaN bounds: reach everything
+    double *o = cols + (size_t)t * kColFields;
+    o[0] = fmin(xa, xb);
+    o[1] = fmax(xa, xb);
+    o[2] = fmin(ya, yb);
+    o[3] = fmax(ya, yb);
+    o[4] = T;
+    o[5] = B;
+    o[6] = Rm;
+}
+
+__global__ __launch_bounds__(256) void k_cull_map_init(unsigned long long *__restrict__ kt,
+                                                       unsigned long long *__restrict__ kb, int nm) {
+    const int t = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (t < nm) {
+        kt[t] = ord_key(-INFINITY);
+        kb[t] = ord_key(INFINITY);
+    }
+}
+
+// map cell (thread) x a chunk of kMapChunk lattice columns (blockIdx.y): the chunk's largest height
+// and lowest depth into the cell's ordered keys
+constexpr int kMapChunk = 256;
+__global__ __launch_bounds__(256) void k_cull_map(const double *__restrict__ cols, int ncol, CullMap m,
+                                                  unsigned long long *__restrict__ kt,
+                                                  unsigned long long *__restrict__ kb) {
+    __shared__ double sc[kMapChunk * kColFields];
+    const int c0 = (int)blockIdx.y * kMapChunk;
+    const int nc = min(kMapChunk, ncol - c0);
+    for (int e = (int)threadIdx.x; e < nc * kColFields; e += 256) sc[e] = cols[(size_t)c0 * kColFields + e];
+    __syncthreads();
+    const int t = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (t >= m.mx * m.my) return;
+    const int cx = t % m.mx, cy = t / m.mx;
+    // the cell's rectangle, widened for the particles' floor() assignment
+    const double ex = 1e-9 * (fabs(m.x0) + m.mx * m.cw) + 1e-300, ey = 1e-9 * (fabs(m.y0) + m.my * m.ch) + 1e-300;
+    // (edge cells reach out to infinity: particles beyond the grid are clamped into them)
+    const double x0 = cx == 0 ? -INFINITY : m.x0 + cx * m.cw - ex;
+    const double x1 = cx == m.mx - 1 ? INFINITY : m.x0 + (cx + 1) * m.cw + ex;
+    const double y0 = cy == 0 ? -INFINITY : m.y0 + cy * m.ch - ey;
+    const double y1 = cy == m.my - 1 ? INFINITY : m.y0 + (cy + 1) * m.ch + ey;
+    double top = -INFINITY, bot = INFINITY;
+    for (int q = 0; q < nc; ++q) {
+        const double *o = sc + q * kColFields;
+        const double gx = fmax(fmax(o[0] - x1, x0 - o[1]), 0.0), gy = fmax(fmax(o[2] - y1, y0 - o[3]), 0.0);
+        const double g2 = gx * gx + gy * gy, R = o[6];
+        if (!(R < INFINITY)) {  // an unbounded lattice cell: keep the whole column
+            top = INFINITY;
+            bot = -INFINITY;
+        } else if (g2 <= R * R) {
+            const double h = sqrt(R * R - g2);
+            const double mgn = 1e-9 * (fabs(o[4]) + fabs(o[5]) + R);
+            top = fmax(top, (o[4] - R) + h + mgn);
+            bot = fmin(bot, (o[5] + R) - h - mgn);
+        }
+    }
+    if (top > -INFINITY) atomicMax(kt + t, ord_key(top));
+    if (bot < INFINITY) atomicMin(kb + t, ord_key(bot));
+}
+
+// decode the keys into the map (top / bot doubles); with `used`, the proof that the cull ran with
+// a map at least as wide everywhere (*fail: 0 = proven; any cell short sets +inf's bits)
+__global__ __launch_bounds__(256) void k_cull_map_final(const unsigned long long *__restrict__ kt,
+                                                        const unsigned long long *__restrict__ kb, int nm,
+                                                        double *__restrict__ top, double *__restrict__ bot,
+                                                        const double *__restrict__ utop,
+                                                        const double *__restrict__ ubot,
+                                                        unsigned long long *__restrict__ fail) {
+    const int t = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    bool short_ = false;
+    if (t < nm) {
+        const double a = ord_val(kt[t]), b = ord_val(kb[t]);
+        top[t] = a;
+        bot[t] = b;
+        if (utop != nullptr) short_ = !(a <= utop[t]) || !(b >= ubot[t]);
+    }
+    if (utop != nullptr && __builtin_amdgcn_ballot_w64(short_) != 0 && (threadIdx.x & 63) == 0)
+        atomicMax(fail, (unsigned long long)__double_as_longlong(INFINITY));
+}
+
+int launch_cull_need(const double *lax, const double *lay, const double *laz, const int n[3], const double *dk,
+                     double mg, const CullMap &m, double *top, double *bot, double *cols, unsigned long long *keys,
+                     const CullMap *used, unsigned long long *fail, hipStream_t s) {
+    const int ncol = std::max(n[0] - 1, 1) * std::max(n[1] - 1, 1);
+    const int nm = m.mx * m.my;
+    hipLaunchKernelGGL(k_cull_columns, dim3((ncol + 255) / 256), dim3(256), 0, s, lax, lay, laz, n[0], n[1], n[2], dk, mg,
+                       cols);
+    hipLaunchKernelGGL(k_cull_map_init, dim3((nm + 255) / 256), dim3(256), 0, s, keys, keys + nm, nm);
+    hipLaunchKernelGGL(k_cull_map, dim3((nm + 255) / 256, (ncol + kMapChunk - 1) / kMapChunk), dim3(256), 0, s,
+                       (const double *)cols, ncol, m, keys, keys + nm);
+    if (used != nullptr) PTV_HIP(hipMemsetAsync(fail, 0, sizeof(unsigned long long), s));
+    hipLaunchKernelGGL(k_cull_map_final, dim3((nm + 255) / 256), dim3(256), 0, s, (const unsigned long long *)keys,
+                       (const unsigned long long *)(keys + nm), nm, top, bot, used ? used->top : nullptr,
+                       used ? used->bot : nullptr, fail);
+    PTV_HIP(hipGetLastError());
+    return PTV_OK;
+}
+
+// a fingerprint of a particle set: the six values of kFingerprint evenly spaced particles
+__global__ void k_fingerprint(Cols6 c, int64_t n, double *__restrict__ out) {
+    const int t = (int)threadIdx.x;
+    if (t < 6 * kFingerprint) {
+        const int a = t / kFingerprint, j = t % kFingerprint;
+        out[t] = c.src[a][(int64_t)((double)j * (double)(n - 1) / (double)(kFingerprint - 1))];
+    }
+}
+
+int launch_fingerprint(const double *const src[6], int64_t n, double *out, hipStream_t s) {
+    Cols6 c;
+    for (int a = 0; a < 6; ++a) {
+        c.src[a] = src[a];
+        c.dst[a] = nullptr;
+    }
+    hipLaunchKernelGGL(k_fingerprint, dim3(1), dim3(6 * kFingerprint), 0, s, c, n, out);
+    PTV_HIP(hipGetLastError());
     return PTV_OK;
 }
 

@@ -26,8 +26,30 @@ size_t scan_partials_needed(size_t m);
 // (pinned; valid after the stream synchronises; NULL: left on the device in bcount[cull_blocks(n)]).
 // Order-preserving.
 size_t cull_blocks(int64_t n);
+// per-column cull map (PTV_FLAG_SLAB_CULL_AUTO): a uniform mx x my grid of (x, y) cells of size
+// cw x ch from (x0, y0); a particle outside the slab's z extent is kept iff its z is <= top[cell]
+// (above the slab) or >= bot[cell] (below) of its cell (clamped to the grid)
+struct CullMap {
+    const double *top = nullptr, *bot = nullptr;
+    int mx = 0, my = 0;
+    double x0 = 0.0, y0 = 0.0, cw = 1.0, ch = 1.0, icw = 1.0, ich = 1.0;
+};
+// map != NULL: the per-column map replaces the scalar halo
 int launch_cull(const double *const src[6], int64_t n, const double *az, int z0, int z1, double halo, double *win,
-                uint32_t *bcount, double *const dst[6], uint32_t *h_total, hipStream_t s);
+                uint32_t *bcount, double *const dst[6], uint32_t *h_total, hipStream_t s,
+                const CullMap *map = nullptr);
+// the map a slab needs, from its finest lattice (axes lax / lay / laz, n[3] points, k-th distance
+// bounds dk over the particles binned): top / bot per cell of m's geometry; cols: 7 (n0-1)(n1-1)
+// doubles and keys: 2 mx my u64 of scratch.  With `used` (the map the binned particles were
+// culled with) *fail is set to 0 when the need fits inside it everywhere (the cull is proven
+// exact), else to +inf's bits (ptv_knn_params.slab_halo's gate convention).
+int launch_cull_need(const double *lax, const double *lay, const double *laz, const int n[3], const double *dk,
+                     double mg, const CullMap &m, double *top, double *bot, double *cols, unsigned long long *keys,
+                     const CullMap *used, unsigned long long *fail, hipStream_t s);
+
+// 6 * kFingerprint doubles identifying a particle set (the cull map cache's key, with n and the arrays)
+constexpr int kFingerprint = 16;
+int launch_fingerprint(const double *const src[6], int64_t n, double *out, hipStream_t s);
 
 // ---- k-NN interpolation (ptv_knn.hip) ----
 // Exact k-th-neighbour distances on a coarser separable lattice (every `step`-th
@@ -48,6 +70,7 @@ constexpr int kModeKDist = 1;   // write the exact k-th neighbour distance into 
 constexpr int kModeSlots = 2;   // write each voxel's k neighbour slots (sorted-record indices)
 constexpr int kModeRadius = 3;  // IDW over every particle within a fixed radius (PTV_METHOD_IDW_RADIUS)
 constexpr int kModeFilter = 4;  // the outlier filter's (k+1)-NN + median/MAD epilogue (filtering.py:20-51)
+constexpr int kModeKDistMerge = 5;  // launcher-internal: k_kdist_merge of a split lattice launch
 
 // kModeFilter inputs / outputs (point-list queries = the particles, ptv_filter.hip layout)
 struct FilterEpilogue {
@@ -88,7 +111,18 @@ struct KnnLaunch {
     // slab cull proof gate (see KnnKernelArgs::gate): NULL = always run
     const unsigned long long *gate = nullptr;
     double gate_halo = 0.0;
+    // kModeKDist with a block order: the first split_blocks blocks of the order run as a split
+    // launch, split waves per tile, merged by k_kdist_merge (ptv_knn_impl.hpp); split_out holds
+    // split_blocks * 4 * split * KMAX * 64 slots (0 = off)
+    int split = 0;
+    int split_blocks = 0;
+    uint32_t *split_out = nullptr;
 };
+
+// the split lattice launch's partial-list buffer (slots) for a KMAX list
+inline size_t kdist_split_slots(int split, int split_blocks, int kmax) {
+    return (size_t)split_blocks * 4 * (size_t)split * (size_t)kmax * 64;
+}
 
 // Longest-first dispatch order for a lattice-level k-NN launch over (nx, ny, nz) points: each
 // block (4 x 1 x 1 tiles of 4^3 points) is keyed by the largest coarser-level bound dk over the

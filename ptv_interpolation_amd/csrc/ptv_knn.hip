@@ -361,6 +361,37 @@ int launch_knn(const KnnLaunch &a, const Binned &b, const double *ax, const doub
     ka.rep_cap = 0;
     ka.tiles = nullptr;
     ka.ntiles = 0;
+    ka.split = 0;
+    ka.split_tiles = 0;
+    ka.split_out = nullptr;
+    if (a.mode == kModeKDist && a.split > 1 && a.split_blocks > 0 && a.order != nullptr && a.split_out != nullptr) {
+        // lattice level: the first split_blocks blocks of the longest-first order (the void tiles)
+        // with `split` waves per tile, the rest of the order as usual, then the merge of the split
+        // tiles' partial lists (k_kdist_merge); parts that find no bound leave their lists cleared
+        const int nsb = (int)std::min<long long>(a.split_blocks, nblocks);
+        KnnKernelArgs ks = ka;
+        ks.split = a.split;
+        ks.split_tiles = nsb * 4;
+        ks.split_out = a.split_out;
+        PTV_HIP(hipMemsetAsync(a.split_out, 0xff, kdist_split_slots(a.split, nsb, km) * sizeof(uint32_t), s));
+        const long long sblocks = ((long long)ks.split_tiles * a.split + 3) / 4;
+        if (sblocks > 0x7fffffffLL) {
+            set_error("split lattice launch too large");
+            return PTV_E_ARG;
+        }
+        ks.nblocks = (int)sblocks;
+        int rc = launch_kmax(km, false, grid_for(sblocks), s, ks, b, ax, ay, az, qx, qy, qz, mask, U, V, W);
+        if (rc != PTV_OK) return rc;
+        if (nblocks > nsb) {
+            KnnKernelArgs kn = ka;
+            kn.order = a.order + nsb;
+            kn.nblocks = (int)(nblocks - nsb);
+            rc = launch_kmax(km, false, grid_for(kn.nblocks), s, kn, b, ax, ay, az, qx, qy, qz, mask, U, V, W);
+            if (rc != PTV_OK) return rc;
+        }
+        ks.mode = kModeKDistMerge;
+        return launch_kmax(km, false, grid_for(nsb), s, ks, b, ax, ay, az, qx, qy, qz, mask, U, V, W);
+    }
     const bool repair = keys && a.mode != kModeKDist && a.mode != kModeRadius;
     if (repair) {
         if (a.rep_cnt == nullptr || a.rep_list == nullptr || a.h_rep == nullptr) {

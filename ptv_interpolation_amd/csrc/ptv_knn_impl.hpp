@@ -128,6 +128,14 @@ struct KnnKernelArgs {
     // launch does nothing unless gate_halo >= proven (the host reads the proof after it)
     const unsigned long long *gate;
     double gate_halo;
+    // lattice void tiles (kModeKDist, see k_kdist_merge): a split launch runs `split` waves per
+    // tile over the first split_tiles tiles of the block order (tile t = block order[t / 4], x-tile
+    // t % 4), wave part p taking every split-th candidate window of one pass at the lattice bound,
+    // and leaves its partial list in split_out[((t * split + p) * KMAX + j) * 64 + lane] (slots,
+    // ~0 = none); 0 = an ordinary launch
+    int split;
+    int split_tiles;
+    uint32_t *split_out;
 };
 
 // Packed keys (the KMAX >= 16 lists).  A key is the candidate's exact f64 d2 with the low B
@@ -593,6 +601,59 @@ __device__ __forceinline__ double axis_gap(int c, double o, double cs, double lo
     return fmax(fmax(c0 - hi, lo - c1), 0.0);
 }
 
+// kModeKDist outputs of a lattice point's final list: an upper bound on its k-th neighbour distance
+// in U[vo] and, with kd_recs, its k nearest records {particle - point (fp32), slot}, which seed the
+// next finer level's tiles (any k distinct particles do: list order need not be exact there).
+// Key lists (KEYS) hold k + 1 entries after the kpad sentinels, pair lists k.
+template <int KMAX, bool KEYS>
+__device__ __forceinline__ void kdist_out(const KnnKernelArgs &a, const double4 *__restrict__ prec,
+                                          const double (&bd)[KMAX], const int (&bp)[KEYS ? 1 : KMAX], double qx,
+                                          double qy, double qz, size_t vo, double *__restrict__ U) {
+    if constexpr (KEYS) {
+        U[vo] = sqrt(bd[KMAX - 2] * a.kscale) * (1.0 + 0x1p-50);
+        if (a.kd_recs != nullptr) {
+            float4 *o = a.kd_recs + vo * (size_t)a.k;
+#pragma unroll
+            for (int j0 = 0; j0 < KMAX; j0 += 8) {  // blocks of 8 gathers in flight
+                double4 rec[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const int j = min(j0 + i, KMAX - 1);
+                    const bool ok = bd[j] >= 0.0 && bd[j] < INFINITY;
+                    rec[i] = prec[ok ? key_slot(bd[j], a.smask) : 0u];
+                }
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const int j = j0 + i;
+                    if (j < KMAX - 1 && j >= a.kpad) {
+                        const bool ok = bd[j] >= 0.0 && bd[j] < INFINITY;
+                        o[j - a.kpad] = make_float4(ok ? (float)(rec[i].x - qx) : 0.f, ok ? (float)(rec[i].y - qy) : 0.f,
+                                                    ok ? (float)(rec[i].z - qz) : 0.f,
+                                                    __uint_as_float(ok ? key_slot(bd[j], a.smask) : 0xffffffffu));
+                    }
+                }
+            }
+        }
+    } else {
+        U[vo] = sqrt(bd[KMAX - 1]);
+        if (a.kd_recs != nullptr) {
+            float4 *o = a.kd_recs + vo * (size_t)a.k;
+            double4 rec[KMAX];
+#pragma unroll
+            for (int j = 0; j < KMAX; ++j) rec[j] = prec[max(bp[j], 0)];  // every load in flight at once
+#pragma unroll
+            for (int j = 0; j < KMAX; ++j) {
+                if (j >= a.kpad) {
+                    const bool ok = bp[j] >= 0;
+                    o[j - a.kpad] = make_float4(ok ? (float)(rec[j].x - qx) : 0.f, ok ? (float)(rec[j].y - qy) : 0.f,
+                                                ok ? (float)(rec[j].z - qz) : 0.f,
+                                                __uint_as_float(ok ? (uint32_t)bp[j] : 0xffffffffu));
+                }
+            }
+        }
+    }
+}
+
 // MODE (kModeInterp / kModeKDist / kModeSlots) is a template parameter so that the search-only
 // modes carry no interpolation epilogue: one kernel for every mode put the KMAX = 32 lists at
 // 284 registers (one wave per SIMD); split, every KMAX <= 32 kernel runs two waves per SIMD.
@@ -659,7 +720,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
     if (a.gate != nullptr && !(__longlong_as_double((long long)*a.gate) <= a.gate_halo))
         return;  // slab cull not proven exact: no outputs (the call returns PTV_E_INEXACT)
     int b, tw;  // block of the tile grid, wave (x-tile) within it
-    if (a.tiles != nullptr) {
+    // split lattice launch: this wave's part of its tile's candidate windows (wave-uniform)
+    int part = 0, nparts = 1;
+    bool split_epi = false;
+    if (MODE == kModeKDist && a.split > 0) {
+        const int e = lb * 4 + wid;
+        const int t = e / a.split;
+        if (t >= a.split_tiles) return;
+        part = __builtin_amdgcn_readfirstlane(e - t * a.split);
+        nparts = a.split;
+        split_epi = true;
+        b = a.order[t >> 2];
+        tw = t & 3;
+    } else if (a.tiles != nullptr) {
         // repair launch: wave e takes the e-th listed tile (wave-uniform exit)
         const int e = lb * 4 + wid;
         if (e >= a.ntiles) return;
@@ -1107,6 +1180,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
         // (coarse level) is preceded by a pass at the density radius r0.
         if (R_ub < INFINITY) R = (seeded || R_ub <= 2.0 * a.r0) ? R_ub : a.r0;
         if constexpr (MODE == kModeRadius) R = a.radius;  // one pass
+        if (nparts > 1) {
+            // split lattice tile: one pass at the bound, which covers every lane's k nearest, so the
+            // merged lists are exact; without a bound the first part searches alone
+            if (R_ub < INFINITY) {
+                R = R_ub;
+            } else {
+                if (part != 0) return;  // its list stays empty (the launcher cleared split_out)
+                nparts = 1;
+            }
+        }
         // ---- sub-balls: the tile's 8 sub-boxes of 2x2x2 voxels (lanes differing in bits 0, 2, 4),
         //      each with centre c_s and radius max_v sqrt(thr_v) + |v - c_s|: a candidate outside
         //      every sub-ball can never enter any list (thresholds only shrink), so the copy drops it.
@@ -1261,6 +1344,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
             const int nyr = 2 * hy + 1;
             const int nrows = nyr * (2 * hz + 1);
             const float inv_nyr = 1.0f / (float)nyr;
+            int wbase = 0;  // candidate windows of this pass's earlier rounds (split launches)
             for (int rb = 0; rb < nrows; rb += 64 * kRowsPerLane) {
                 ++n_round;
                 // ---- lane = kRowsPerLane cell rows: x-runs of this shell -> particle ranges ----
@@ -1382,17 +1466,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                     }
                     return sl;
                 };
-                uint32_t next_slot = total > 0 ? window_slot(0) : 0u;
+                // this wave's windows: every one, or (split launch) those whose index within the
+                // pass is congruent to its part modulo the parts
+                const int wstride = 64 * nparts;
+                const int src0 = 64 * ((part - wbase % nparts + nparts) % nparts);
+                wbase += (total + 63) >> 6;
+                uint32_t next_slot = src0 < total ? window_slot(src0) : 0u;
                 double4 next_rec = prec[next_slot];
                 // the pass's last round runs at least one (possibly empty) window, so that the
                 // final flush below is the loop's own (one inlined copy of the insert network)
                 const bool last_round = rb + 64 * kRowsPerLane >= nrows;
-                const int tot_it = (total == 0 && last_round) ? 1 : total;
-                for (int src = 0; src < tot_it; src += 64) {
+                const int tot_it = last_round ? max(total, src0 + 1) : total;
+                for (int src = src0; src < tot_it; src += wstride) {
                     const uint32_t slot = next_slot;
                     const double4 p4 = next_rec;
-                    if (src + 64 < total) {
-                        next_slot = window_slot(src + 64);
+                    if (src + wstride < total) {
+                        next_slot = window_slot(src + wstride);
                         next_rec = prec[next_slot];
                     }
                     const int i = src + lane;
@@ -1425,16 +1514,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                         fbz[pos] = ez;
                     }
                     nbuf += __builtin_popcountll(km);
-                    n_cand += (uint32_t)min(64, total - src);
+                    n_cand += (uint32_t)max(0, min(64, total - src));
                     stamp(t_copy);
-                    if (nbuf > kCap - 64 || (last_round && src + 64 >= tot_it)) flush();
+                    if (nbuf > kCap - 64 || (last_round && src + wstride >= tot_it)) flush();
                 }
             }
             // ---- exactness: lanes with k-th distance <= R are final ----
             // (key lists: the key bound covers every candidate sharing the k-th key's truncation,
             // so the (k+1)-th slot sees them all too)
             const double worst = uniform(wave_max(kth2()));  // inactive lanes hold -1
-            if (MODE == kModeRadius || worst <= R * R || R >= a.rall) break;
+            if (MODE == kModeRadius || worst <= R * R || R >= a.rall || nparts > 1) break;
             Rp = R;
             py0 = ry0;
             py1 = ry1;
@@ -1496,53 +1585,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
         return (dx * dx + dy * dy) + dz * dz;
     };
     if constexpr (MODE == kModeKDist) {
-        if constexpr (KEYS) {
-            // an upper bound on the k-th distance (the lattice only ever needs one)
-            U[vo] = sqrt(kth2()) * (1.0 + 0x1p-50);
-            if (a.kd_recs != nullptr) {
-                // the first k entries' records seed the next finer level (any k distinct particles
-                // do: list order need not be exact here), in blocks of 8 gathers
-                float4 *o = a.kd_recs + vo * (size_t)a.k;
+        if (split_epi) {
+            // split lattice tile: this part's list (slots, ~0 = none) for k_kdist_merge
+            uint32_t *o = a.split_out + (size_t)(lb * 4 + wid) * KMAX * 64 + lane;
 #pragma unroll
-                for (int j0 = 0; j0 < KMAX; j0 += 8) {
-                    double4 rec[8];
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) {
-                        const int j = min(j0 + i, KMAX - 1);
-                        const bool ok = bd[j] >= 0.0 && bd[j] < INFINITY;
-                        rec[i] = prec[ok ? key_slot(bd[j], a.smask) : 0u];
-                    }
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) {
-                        const int j = j0 + i;
-                        if (j < KMAX - 1 && j >= a.kpad) {
-                            const bool ok = bd[j] >= 0.0 && bd[j] < INFINITY;
-                            o[j - a.kpad] = make_float4(ok ? (float)(rec[i].x - qx) : 0.f, ok ? (float)(rec[i].y - qy) : 0.f,
-                                                        ok ? (float)(rec[i].z - qz) : 0.f,
-                                                        __uint_as_float(ok ? key_slot(bd[j], a.smask) : 0xffffffffu));
-                        }
-                    }
-                }
+            for (int j = 0; j < KMAX; ++j) {
+                if constexpr (KEYS) o[j * 64] = (bd[j] >= 0.0 && bd[j] < INFINITY) ? key_slot(bd[j], a.smask) : 0xffffffffu;
+                else o[j * 64] = bp[j] >= 0 ? (uint32_t)bp[j] : 0xffffffffu;
             }
         } else {
-            U[vo] = sqrt(bd[KMAX - 1]);
-            if (a.kd_recs != nullptr) {
-                // the k-NN records (list order) seed the next finer level's tiles: {p - this lattice
-                // point in fp32, slot}
-                float4 *o = a.kd_recs + vo * (size_t)a.k;
-                double4 rec[KMAX];
-#pragma unroll
-                for (int j = 0; j < KMAX; ++j) rec[j] = prec[max(bp[j], 0)];  // every load in flight at once
-#pragma unroll
-                for (int j = 0; j < KMAX; ++j) {
-                    if (j >= a.kpad) {
-                        const bool ok = bp[j] >= 0;
-                        o[j - a.kpad] = make_float4(ok ? (float)(rec[j].x - qx) : 0.f, ok ? (float)(rec[j].y - qy) : 0.f,
-                                                    ok ? (float)(rec[j].z - qz) : 0.f,
-                                                    __uint_as_float(ok ? (uint32_t)bp[j] : 0xffffffffu));
-                    }
-                }
-            }
+            kdist_out<KMAX, KEYS>(a, prec, bd, bp, qx, qy, qz, vo, U);
         }
         write_stamps();
         return;
@@ -2240,6 +2292,54 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
     }  // exact-pair lists
 }
 
+// Lattice void tiles.  A 4x4x4-point lattice tile inside a large solid sphere of the pack gathers
+// the particle shell around it (~59k candidates at 512^3 / 5M) in one wave: 1.7 of the 1.8 ms
+// lattice level, on the critical path of every launch and z-slab that holds it.  The launcher runs
+// the first tiles of the longest-first block order as a split launch (KnnKernelArgs::split: S
+// waves per tile, each taking every S-th candidate window of one pass at the lattice bound, which
+// covers every lane's k nearest) and merges the S partial lists here: one wave per tile, lane =
+// lattice point, each listed slot's exact d2 recomputed (bit-identical to the search's) and
+// inserted into a fresh list.  The k smallest of the union are the k smallest of the parts' k
+// smallest, so the k-th distance (the bound every finer level uses) is the unsplit launch's.
+template <int KMAX>
+__global__ __launch_bounds__(256) void k_kdist_merge(KnnKernelArgs a, const double4 *__restrict__ prec,
+                                                     const double *__restrict__ ax, const double *__restrict__ ay,
+                                                     const double *__restrict__ az, double *__restrict__ U) {
+    constexpr bool KEYS = kKeyList<KMAX, false>;
+    const int lane = threadIdx.x & 63;
+    const int t = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+    if (t >= a.split_tiles) return;  // wave-uniform
+    const int b = a.order[t >> 2], tw = t & 3;
+    const int bx = b % a.ntxb, rr = b / a.ntxb;
+    const int ty = rr % a.nty, tz = rr / a.nty;
+    const int tx = bx * 4 + tw;
+    if (tx >= a.ntx) return;
+    const int ix = tx * 4 + (lane & 3), iy = ty * 4 + ((lane >> 2) & 3), iz = a.z0 + tz * 4 + (lane >> 4);
+    if (!(ix < a.nx && iy < a.ny && iz < a.z1)) return;
+    const size_t vo = ((size_t)(iz - a.z0) * a.ny + iy) * a.nx + ix;
+    const double qx = ax[ix], qy = ay[iy], qz = az[iz];
+    double bd[KMAX];
+    int bp[KEYS ? 1 : KMAX];
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) bd[j] = j < a.kpad ? -1.0 : INFINITY;
+#pragma unroll
+    for (int j = 0; j < (KEYS ? 1 : KMAX); ++j) bp[j] = -1;
+    const uint32_t *in = a.split_out + (size_t)t * a.split * KMAX * 64 + lane;
+    for (int p = 0; p < a.split; ++p) {
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+            const uint32_t sl = in[((size_t)p * KMAX + j) * 64];
+            const bool has = sl != 0xffffffffu;
+            const double4 c = prec[has ? sl : 0u];
+            const double dx = qx - c.x, dy = qy - c.y, dz = qz - c.z;
+            const double e2 = (dx * dx + dy * dy) + dz * dz;
+            if constexpr (KEYS) insert_key<KMAX>(bd, make_key(has, e2, has ? sl : 0u, a.smask));
+            else insert<KMAX>(bd, bp, has ? e2 : INFINITY, (int)sl);  // +inf: a no-op
+        }
+    }
+    kdist_out<KMAX, KEYS>(a, prec, bd, bp, qx, qy, qz, vo, U);
+}
+
 template <int KMAX, int MODE, bool EXACT>
 void launch_m(dim3 grid, hipStream_t s, const KnnKernelArgs &ka, const Binned &b, const double *ax,
                      const double *ay, const double *az, const double *qx, const double *qy, const double *qz,
@@ -2267,6 +2367,10 @@ void launch_t(dim3 grid, hipStream_t s, const KnnKernelArgs &ka, const Binned &b
     switch (ka.mode) {
         case kModeKDist:
             if constexpr (!EXACT) launch_m<KMAX, kModeKDist, false>(grid, s, ka, b, ax, ay, az, qx, qy, qz, mask, U, V, W);
+            break;
+        case kModeKDistMerge:
+            if constexpr (!EXACT)
+                hipLaunchKernelGGL((k_kdist_merge<KMAX>), grid, dim3(256), 0, s, ka, b.prec, ax, ay, az, U);
             break;
         case kModeSlots: launch_m<KMAX, kModeSlots, EXACT>(grid, s, ka, b, ax, ay, az, qx, qy, qz, mask, U, V, W); break;
         case kModeRadius:

@@ -25,9 +25,10 @@
 // Anything outside that regime is flagged per voxel and re-solved by the pivoting kernel
 // (k_rbf_local in list mode, the host launches it right after this kernel): a rank-deficient
 // polynomial block (|Rt_tt| < 1e-9 sqrt(k): coplanar / collinear neighbourhoods, where LAPACK
-// decides singularity), a pivot of B that is not positive or outside the Newton reciprocal's
-// range, a negative per-point smoothing, non-finite inputs.  So singular systems keep the
-// pivoting kernel's (and LAPACK's) verdict.
+// decides singularity), a pivot of B at or below 2^-40 of B's largest diagonal entry (singular to
+// working precision: coincident neighbours) or outside the Newton reciprocal's range, a negative
+// per-point smoothing, non-finite inputs.  So singular systems keep the pivoting kernel's (and
+// LAPACK's) verdict.
 //
 // Layout (per wave: four systems, one per 16-lane row; lane li holds system rows li + 16 q,
 // q < R, in registers):
@@ -217,7 +218,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     constexpr int MS = NC + 1;
     constexpr int SCS = FULL ? 4 * NC * MS : 4 * NC * Bd::HS;
     constexpr int SVS = 4 * NC * 8;  // sorted (values, yhat) double4 pairs per wave
-    constexpr int SRS = NP * R * 64 + 4 * 2 * NP;   // reflectors (per lane) + tau, beta (per system)
+    constexpr int SRS = NP * R * 64 + 4 * (2 * NP + 1);  // reflectors (per lane) + tau, beta, pivot tolerance (per system)
     constexpr int SC0 = SCS > SVS ? SCS : SVS;
     constexpr int SC = SC0 > SRS ? SC0 : SRS;
     __shared__ double4 s_ye[4][4][NC];  // per wave and system: eps-scaled coordinates + id, id order
@@ -515,8 +516,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     rbf_wave_sync();  // every lane has its rows: the scratch now keeps the reflectors for step 8
     if constexpr (PFR) stage2(li);  // prefetch, stage 2: the next quad's particle records
     double *vst = sc;                                  // V[t][q] at vst[(t * R + q) * 64 + lane]
-    double *tbs = sc + NP * R * 64 + seg * (2 * NP);  // tau[t], beta[t] of this system
-    static_assert(NP * R * 64 + 4 * 2 * NP <= SC, "reflector store fits the scratch");
+    double *tbs = sc + NP * R * 64 + seg * (2 * NP + 1);  // tau[t], beta[t], pivot tolerance of this system
+    static_assert(SRS <= SC, "reflector store fits the scratch");
 #pragma unroll
     for (int t = 0; t < NP; ++t) {
 #pragma unroll
@@ -557,6 +558,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 #pragma unroll
         for (int q = 0; q < R; ++q) Y[t][q] = fma(-kk, Vr[t][q], Y[t][q]);  // z_t
     }
+    // the projected block's largest diagonal entry, B_jj = Phi_jj - 2 sum_t v_t[j] z_t[j] over this
+    // lane's rows NP <= j < k: the scale of the relative pivot test in step 5
+    double dgb = 0.0;
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        const int row = li + 16 * q;
+        double bjj = dg[q];
+#pragma unroll
+        for (int t = 0; t < NP; ++t) bjj = fma(-2.0 * Vr[t][q], Y[t][q], bjj);
+        dgb = row >= NP && row < k ? fmax(dgb, bjj) : dgb;
+    }
+    // a pivot at or below 2^-40 of it: the block is singular to working precision (coincident
+    // neighbours make it exactly singular, e_i - e_j lies in the null space of P^T and of Phi, and
+    // rounding leaves a last pivot of ~1e-16 relative and either sign), so the voxel goes to the
+    // pivoting kernel, which meets LAPACK's verdict; a legitimate system with cond ~1e8 keeps
+    // pivots near 1e-8 of it.  Kept in LDS (tested against the reciprocals after step 6: a register
+    // live across the LU spills at 32 slots)
+    dgb = 0x1p-40 * seg_max<16>(dgb);
+    if (li == 0) tbs[2 * NP] = dgb;
     double nV[NP][R], nY[NP][R];  // negated: A += nY v[j] + nV z[j], each an fmac with the broadcast folded
 #pragma unroll
     for (int t = 0; t < NP; ++t)
@@ -662,6 +682,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 
     // ---- 7. Rt e = rhs (rows 0..NP-1: lanes 0..NP-1; Rt_it = P[0][t] of lane i < t, diag beta) ----
     rbf_wave_sync();  // the reflector store is read back from here on
+    {
+        // the relative pivot test of step 4's tolerance: piv <= tol <=> 1/piv >= 1/tol (piv > 0 by now)
+        const double ptol = tbs[2 * NP];
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const int row = li + 16 * q;
+            if (row >= NP && row < k) bad = bad || !(rd[q] * ptol < 1.0);
+        }
+    }
     double E[3] = {0.0, 0.0, 0.0}, rh[3] = {B[0][0], B[0][1], B[0][2]};
 #pragma unroll
     for (int t = NP - 1; t >= 0; --t) {

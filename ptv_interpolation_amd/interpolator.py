@@ -262,29 +262,17 @@ def _knn_field(points, values, grid_tuple, method, k, power, radius=0.0):
     axes = separable_axes(X, Y, Z)
     if axes is not None:
         # z-slab per device (launcher.py); bit-identical to one whole-grid call.  With several
-        # slabs each one bins only the particles within a halo of its planes (slab_halo: the library
-        # proves the cull exact from its lattice bounds or says which halo would be; interp_slab
-        # retries with it), as the north_star z-slab partition does (zslab.py)
-        from . import zslab
-
+        # slabs each one bins only the particles that can reach its planes (PTV_FLAG_SLAB_CULL_AUTO:
+        # a per-column cull map the slab's context derives from its own lattice bounds on the first
+        # call and proves exact on the device on every later call with the same particles), as the
+        # north_star z-slab partition does (zslab.py)
         nz = len(axes[2])
-        halo0 = 0.0
-        if launcher.slab_count(nz) > 1 and method != "idw_radius":
-            halo0 = zslab.halo_guess(n, [float(np.max(a) - np.min(a)) for a in axes], k)
+        flags = _lib.FLAG_SLAB_CULL_AUTO if (launcher.slab_count(nz) > 1 and method != "idw_radius") else 0
 
         def slab(ctx, z0, z1, views):
-            def call(h):
-                ctx.interp_knn(points, values, axes=axes, method=m, k=k, power=power, eps=_EPS, z_range=(z0, z1),
-                               out=views, radius=radius, slab_halo=h)
-                return ctx.stats
-
-            if halo0 <= 0.0:
-                return call(0.0)
-            hs = zslab.HaloState(halo0)
-            st = dict(zslab.interp_slab(call, hs))
-            st["halo_state"] = hs.as_dict()  # the halo tried first / last, and the retries
-            st["halo_first"] = halo0
-            return st
+            ctx.interp_knn(points, values, axes=axes, method=m, k=k, power=power, eps=_EPS, z_range=(z0, z1),
+                           out=views, radius=radius, flags=flags)
+            return dict(ctx.stats)
 
         full = [np.empty((nz, len(axes[1]), len(axes[0]))) for _ in range(3)]
         U, V, W = launcher.run_slabs(nz, slab, full)

@@ -5,9 +5,9 @@ Every voxel depends only on the particle set and its own coordinate, and a z-sla
 the kernels produces the same bits as the same planes of a whole-grid call, so the grid's
 z planes are split into contiguous slabs, one per device, each device interpolates its slab
 from the (replicated) particle set, and the slabs land in disjoint slices of the caller's
-output.  The k-NN methods bin only the particles near their slab (ptv_knn_params.slab_halo,
-proven exact from the coarse-lattice bounds, zslab.interp_slab's retry when it is not).  One
-host thread per device drives its own context and stream (ctypes releases the GIL during the C
+output.  The k-NN methods bin only the particles that can reach their slab (the per-column cull
+map of PTV_FLAG_SLAB_CULL_AUTO, cached in each slab's context and proven exact on the device).
+One host thread per device drives its own context and stream (ctypes releases the GIL during the C
 calls); no collective touches the data path.
 
 Devices: ``PTV_DEVICE=i`` pins one device; ``PTV_DEVICES=0,1,...`` lists them (a device
@@ -25,7 +25,15 @@ from . import _lib
 
 _ctx_lock = threading.Lock()
 _slab_ctx = {}
-last_results = []  # what fn returned for each slab of the last run_slabs call (slab order)
+_tls = threading.local()  # per calling thread: what fn returned for each slab of its last run_slabs
+
+
+def __getattr__(name):
+    # launcher.last_results: the calling thread's last run_slabs results (slab order); thread-local,
+    # so concurrent interpolate_field calls do not overwrite each other's per-slab stats
+    if name == "last_results":
+        return getattr(_tls, "results", [])
+    raise AttributeError(name)
 
 
 def devices():
@@ -55,21 +63,24 @@ def context(device: int, slot: int) -> "_lib.Context":
     return c
 
 
-def run_slabs(nz: int, fn, out):
+def run_slabs(nz: int, fn, out, results=None):
     """Fill the preallocated C-contiguous (nz, ...) arrays ``out`` slab by slab.
 
     ``fn(ctx, z0, z1, views)`` writes planes [z0, z1) into ``views`` (the z-slices of ``out``,
     contiguous, written in place by the library's D2H: no per-slab arrays and no host
     concatenation).  One slab per device of ``devices()``, one host thread each; a single
-    device runs fn(ctx, 0, nz, out) directly.  Returns ``out``."""
+    device runs fn(ctx, 0, nz, out) directly.  Returns ``out``; fn's per-slab results are
+    ``last_results`` of the calling thread (or appended to ``results`` when given)."""
     out = tuple(out)
     for a in out:
         if not (a.flags.c_contiguous and a.shape[0] == nz):
             raise ValueError("run_slabs: outputs must be C-contiguous with nz leading planes")
-    global last_results
     devs = devices()
     if len(devs) <= 1 or nz < 2:
-        last_results = [fn(_lib.Context.get(devs[0]), 0, nz, out)]
+        res = [fn(_lib.Context.get(devs[0]), 0, nz, out)]
+        _tls.results = res
+        if results is not None:
+            results.extend(res)
         return out
     slabs = slab_bounds(nz, len(devs))
     seen = {}
@@ -79,7 +90,10 @@ def run_slabs(nz: int, fn, out):
         seen[d] = slot + 1
         jobs.append((context(d, slot), z0, z1, tuple(a[z0:z1] for a in out)))
     with ThreadPoolExecutor(len(jobs)) as ex:
-        last_results = list(ex.map(lambda j: fn(*j), jobs))
+        res = list(ex.map(lambda j: fn(*j), jobs))
+    _tls.results = res
+    if results is not None:
+        results.extend(res)
     return out
 
 

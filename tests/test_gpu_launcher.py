@@ -40,10 +40,10 @@ def test_slabs_on_three_contexts_equal_one_call(monkeypatch, method, kw):
                                        ("sibson", {"sibson_neighbors": 30})])
 def test_slabs_cull_their_particles(monkeypatch, method, kw):
     """The drop-in multi-device path (main.py:184-192 -> interpolate_field -> launcher.run_slabs)
-    bins only the particles within a proven-exact halo of each slab (slab_halo +
-    zslab.interp_slab), not the whole set on every device: PTV_DEVICES=0,0,0,0 (four slabs on
-    four contexts) bins fewer particles than N per slab and reproduces the one-call result bit
-    for bit."""
+    culls each slab's particles with the per-column map of PTV_FLAG_SLAB_CULL_AUTO: the first call
+    of each slab context bins every particle and builds the map from the slab's lattice bounds; the
+    repeated call bins fewer than N per slab (the cull proven exact on the device) and both
+    reproduce the one-call result bit for bit.  PTV_DEVICES=0,0,0,0: four slabs on four contexts."""
     from ptv_interpolation_amd import interpolator as ip
     from ptv_interpolation_amd import launcher, synth
 
@@ -57,10 +57,49 @@ def test_slabs_cull_their_particles(monkeypatch, method, kw):
         assert launcher.last_results[0]["n_binned"] == N
         monkeypatch.delenv("PTV_DEVICE")
         monkeypatch.setenv("PTV_DEVICES", "0,0,0,0")
-        four = ip.interpolate_field(_df(P, Q), (X, Y, Z), method=method, **kw)
-    binned = [st["n_binned"] for st in launcher.last_results]
-    print(f"{method} {kw}: particles binned per slab {binned} of {N}; halos "
-          f"{[(round(st['halo_first'], 2), st['halo_state']) for st in launcher.last_results]}")
+        first = ip.interpolate_field(_df(P, Q), (X, Y, Z), method=method, **kw)
+        binned_first = [st["n_binned"] for st in launcher.last_results]
+        again = ip.interpolate_field(_df(P, Q), (X, Y, Z), method=method, **kw)
+        binned = [st["n_binned"] for st in launcher.last_results]
+    print(f"{method} {kw}: particles binned per slab {binned_first} (first call), {binned} (again) of {N}")
     assert len(binned) == 4 and all(b < N for b in binned)
-    for a, b in zip(four, one):
+    for a, b, c in zip(first, again, one):
+        assert np.array_equal(a, c, equal_nan=True) and np.array_equal(b, c, equal_nan=True)
+
+
+def test_slab_cull_map_refreshes_when_particles_change(monkeypatch):
+    """The cull map is cached per context and keyed by the particle set (arrays, n, a fingerprint):
+    a call with different particles of the same count through the same host-path buffers does not
+    reuse a stale map (or, if the fingerprint missed the change, its proof fails and the call reruns
+    unculled), so the result stays bit-identical to the one-call result."""
+    from ptv_interpolation_amd import interpolator as ip
+    from ptv_interpolation_amd import synth
+
+    G = 96
+    N = 150_000
+    P, Q = synth.sphere_pack(N, G, values="normal")
+    P2 = P.copy()
+    P2[:, 2] = (G - 1) - P2[:, 2]  # the same count, mirrored in z
+    (X, Y, Z), _ = ip.create_grid(((0, G),) * 3, G)
+    with contextlib.redirect_stdout(io.StringIO()):
+        monkeypatch.setenv("PTV_DEVICE", "0")
+        one = ip.interpolate_field(_df(P2, Q), (X, Y, Z), method="idw", idw_neighbors=8)
+        monkeypatch.delenv("PTV_DEVICE")
+        monkeypatch.setenv("PTV_DEVICES", "0,0,0")
+        ip.interpolate_field(_df(P, Q), (X, Y, Z), method="idw", idw_neighbors=8)
+        ip.interpolate_field(_df(P, Q), (X, Y, Z), method="idw", idw_neighbors=8)
+        three = ip.interpolate_field(_df(P2, Q), (X, Y, Z), method="idw", idw_neighbors=8)
+        # the same fingerprint (the 16 sampled particles kept) over changed data: the proof fails
+        # and the call reruns with every particle binned
+        P3 = P2.copy()
+        keep = np.array([int(j * (N - 1) / 15) for j in range(16)])
+        moved = np.setdiff1d(np.arange(N), keep)
+        P3[moved, 2] = (G - 1) - P3[moved, 2]
+        monkeypatch.setenv("PTV_DEVICE", "0")
+        one3 = ip.interpolate_field(_df(P3, Q), (X, Y, Z), method="idw", idw_neighbors=8)
+        monkeypatch.delenv("PTV_DEVICE")
+        three3 = ip.interpolate_field(_df(P3, Q), (X, Y, Z), method="idw", idw_neighbors=8)
+    for a, b in zip(three, one):
+        assert np.array_equal(a, b, equal_nan=True)
+    for a, b in zip(three3, one3):
         assert np.array_equal(a, b, equal_nan=True)

@@ -409,3 +409,88 @@ def test_persistent_kernels_on_tiny_grids(ctx, shape, kernel, k, eps, degree):
     for a, b in zip(got, ref):
         assert a.shape == (nz, ny, nx)
         assert normwise(a, b) <= TOL_ILL if kernel == "gaussian" else normwise(a, b) <= TOL
+
+
+def _interior_biased_voxels(G, n, rng, frac_inside=0.4):
+    """n voxel indices of a G^3 sphere-pack grid, at least `frac_inside` of them inside the solid
+    spheres (void voxels: their neighbourhoods come from a sphere shell), the rest uniform."""
+    from ptv_interpolation_amd import synth
+
+    scale = (G - 1) / (synth.HI - synth.LO)
+    inside = np.empty(0, dtype=np.int64)
+    while inside.size < int(n * frac_inside):
+        c = rng.integers(0, G ** 3, 20 * n)
+        iz, iy, ix = np.unravel_index(c, (G, G, G))
+        dom = synth.LO + np.stack([ix, iy, iz], -1) / scale
+        inside = np.concatenate([inside, c[synth.inside_spheres(dom[:, 0], dom[:, 1], dom[:, 2])]])
+    inside = inside[: int(n * frac_inside)]
+    return np.concatenate([inside, rng.integers(0, G ** 3, n - inside.size)])
+
+
+@pytest.mark.parametrize("kernel,k,G,n", [
+    ("thin_plate_spline", 20, 512, 5_000_000),  # main.py:34-35 default, the rbf_tps20 bench line
+    ("thin_plate_spline", 32, 512, 5_000_000),  # the rbf_tps32 bench line
+    ("quintic", 22, 256, 1_000_000),            # ten monomials, the worst-conditioned family
+    ("cubic", 14, 256, 1_000_000),              # 16 row slots
+])
+def test_nullspace_sphere_pack_sampled(ctx, kernel, k, G, n):
+    """k_rbf_ns on the geometry it is benched on: the whole sphere-pack grid on the GPU, 3000
+    voxels (40 % inside the solid spheres, where the neighbourhoods are sphere-shell caps) against
+    the oracle's LAPACK gesv and the extended-precision solve of the same systems.  Bar per
+    component: gpu-vs-exact <= max(1e-10, lapack-vs-exact).  The voxels handed to the pivoting
+    kernel (n_rbf_pivoted) are printed and bounded."""
+    from oracle import cpu_ref
+    from ptv_interpolation_amd import synth
+    from ptv_interpolation_amd.rbf import LocalRBFInterpolator
+
+    P, Q = synth.sphere_pack(n, G, values="normal")
+    ax = np.linspace(0, G - 1, G)
+    it = LocalRBFInterpolator(P, Q, neighbors=k, kernel=kernel)
+    out = it.evaluate_grid(ax, ax, ax)
+    npiv = ctx.stats["n_rbf_pivoted"]
+    print(f"{kernel} k={k} {G}^3/{n}: voxels handed to the pivoting kernel {npiv} ({npiv / G ** 3:.2e})")
+    assert npiv <= 1e-4 * G ** 3
+    rng = np.random.default_rng(4242 + k)
+    sel = _interior_biased_voxels(G, 3000, rng)
+    iz, iy, ix = np.unravel_index(sel, (G, G, G))
+    q = np.stack([ax[ix], ax[iy], ax[iz]], -1)
+    lap = cpu_ref.rbf_local_points(P, Q, q, k, kernel)
+    ext = cpu_ref.rbf_local_points(P, Q, q, k, kernel, solver="extended")
+    for c, a in enumerate(out):
+        got = a.ravel()[sel]
+        e_ref, e_exact, gap = normwise(got, lap[:, c]), normwise(got, ext[:, c]), normwise(lap[:, c], ext[:, c])
+        print(f"{kernel} k={k} {'UVW'[c]}: gpu-vs-lapack {e_ref:.3e}  gpu-vs-exact {e_exact:.3e}  "
+              f"lapack-vs-exact {gap:.3e}")
+        assert e_exact <= max(TOL, gap)
+
+
+def test_nullspace_coincident_neighbours_take_pivoting_verdict(ctx):
+    """A particle duplicated at the same position makes every system whose k nearest hold both
+    copies exactly singular (e_i - e_j lies in the null space of P^T and of Phi).  The null-space
+    solver's last pivot then comes out ~1e-16 relative with either sign; the relative pivot test
+    hands such voxels to the pivoting kernel, so the default path reaches the same verdict as
+    PTV_FLAG_RBF_PIVOTING (LAPACK's: an exactly zero pivot, LinAlgError)."""
+    from ptv_interpolation_amd import _lib
+    from ptv_interpolation_amd.rbf import LocalRBFInterpolator
+
+    rng = np.random.default_rng(99)
+    cloud = rng.uniform(0, 12, (3000, 3))
+    P = np.concatenate([cloud, cloud[:1]])
+    P[-1] = P[0]
+    Q = rng.standard_normal((len(P), 3))
+    ax = np.linspace(0, 11, 12)
+    verdicts = []
+    for flags in (0, _lib.FLAG_RBF_PIVOTING):
+        try:
+            LocalRBFInterpolator(P, Q, neighbors=20).evaluate_grid(ax, ax, ax, flags=flags)
+            verdicts.append("solved")
+        except np.linalg.LinAlgError:
+            verdicts.append("singular")
+        if flags == 0:
+            npiv = ctx.last_stats()["n_rbf_pivoted"]
+            print("voxels handed to the pivoting kernel:", npiv)
+            assert npiv > 0
+    assert verdicts == ["singular", "singular"]
+    # without the duplicate (the same cloud) nothing is handed over and the result is finite
+    U, V, W = LocalRBFInterpolator(cloud, Q[:-1], neighbors=20).evaluate_grid(ax, ax, ax)
+    assert ctx.last_stats()["n_rbf_pivoted"] == 0 and np.isfinite(U).all()
