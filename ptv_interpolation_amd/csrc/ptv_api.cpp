@@ -307,10 +307,15 @@ constexpr long long kMaxCells = 1LL << 28;
 constexpr long long kLatticeStopPoints = 50000; // no coarser lattice below this many points
 constexpr size_t kSeedBytesMax = 40ULL << 30;    // lattice seed records per level (C5 2048^3, k = 8: 17 GB)
 // split lattice launch (k_kdist_merge): the first max(kLatticeSplitMinBlocks, blocks /
-// kLatticeSplitDiv) blocks of a lattice level's longest-first order, kLatticeSplit waves per tile
+// kLatticeSplitDiv) blocks of a lattice level's longest-first order, kLatticeSplit waves per tile.
+// Measured (512^3 / 5M sphere pack, k = 8, tools/gpu_sweep.sh): the share 2/8 lattice 1.81 ->
+// 0.88 ms at 64 blocks (1.07 at 32, 2.05 at 8), C2 0.81 -> 0.69; the whole 512^3 grid's lattice
+// launch is throughput-bound (35.9k tiles of ~280k cycles each), 1.91 -> 1.86 ms
 constexpr int kLatticeSplit = 16;
-constexpr long long kLatticeSplitMinBlocks = 8;
+constexpr long long kLatticeSplitMinBlocks = 64;
 constexpr long long kLatticeSplitDiv = 128;
+// relative widening of the cached slab cull map over the need it was built from
+constexpr double kCullMapSlack = 1e-6;
 
 int validate(const ptv_particles *p, const ptv_grid *g, const void *prm) {
     if (!p || !g || !prm) {
@@ -450,7 +455,7 @@ struct SearchParams {
 // Fills `kl` with a launch template for planes [z_begin, z_end) of the grid.
 int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchParams *prm, const double *ax,
             const double *ay, const double *az, const double *qx, const double *qy, const double *qz, hipStream_t s,
-            KnnLaunch &kl, Binned &bout, const double *known_bbox = nullptr) {
+            KnnLaunch &kl, Binned &bout, const double *known_bbox = nullptr, bool exact_finest = false) {
     const int64_t n = p->n;
     const bool sep = ax != nullptr;
     const int64_t plane = g->nx * g->ny;
@@ -530,7 +535,10 @@ int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchP
             const long long pts = (long long)n[0] * n[1] * n[2];
             long long stop = kLatticeStopPoints;
             if (const char *e = dev_knob("PTV_LAT_STOP")) stop = std::atoll(e);  // dev override
-            if (pts <= stop || std::min(n[0], std::min(n[1], n[2])) < 9) break;
+            const int nmin = std::min(n[0], std::min(n[1], n[2]));
+            // exact_finest (the slab cull map): a count-bound level above the finest, which is then an
+            // exact k-th distance level (its bounds do not depend on the binning cells)
+            if ((pts <= stop || nmin < 9) && !(exact_finest && nlat == 1 && nmin >= 2)) break;
             Lat &L = lat[nlat];
             for (int d = 0; d < 3; ++d) L.n[d] = n[d] <= 1 ? 1 : (n[d] - 1 + kLatticeStep - 1) / kLatticeStep + 1;
             PTV_TRY(c->lat_axes[nlat].ensure((size_t)L.n[0] + L.n[1] + L.n[2]));
@@ -590,6 +598,22 @@ int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchP
             PTV_TRY(launch_block_order(lat[l + 1].dk, lat[l + 1].n, lat[l].n[0], lat[l].n[1], lat[l].n[2], kl.r0,
                                        c->lat_order[l].p, s));
             ll.order = c->lat_order[l].p;
+            if (const char *e = dev_knob("PTV_DBG_ORDER")) {  // dev builds: the order and the coarser bounds
+                if (l == 0) {
+                    const size_t nc = (size_t)lat[1].n[0] * lat[1].n[1] * lat[1].n[2];
+                    std::vector<int> ho((size_t)nb);
+                    std::vector<double> hd(nc);
+                    PTV_HIP(hipMemcpyAsync(ho.data(), ll.order, nb * sizeof(int), hipMemcpyDeviceToHost, s));
+                    PTV_HIP(hipMemcpyAsync(hd.data(), lat[1].dk, nc * sizeof(double), hipMemcpyDeviceToHost, s));
+                    PTV_HIP(hipStreamSynchronize(s));
+                    if (FILE *f = std::fopen(e, "wb")) {
+                        std::fwrite(lat[1].n, sizeof(int), 3, f);
+                        std::fwrite(hd.data(), sizeof(double), nc, f);
+                        std::fwrite(ho.data(), sizeof(int), ho.size(), f);
+                        std::fclose(f);
+                    }
+                }
+            }
             // the first blocks of the order (the void tiles) as a split launch (k_kdist_merge)
             int split = kLatticeSplit;
             long long sblk = std::min<long long>(nb, std::max<long long>(kLatticeSplitMinBlocks, nb / kLatticeSplitDiv));
@@ -631,6 +655,19 @@ int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchP
     }
     PTV_HIP(hipEventRecord(c->ev_lat1, s));
     PTV_HIP(hipEventRecord(c->ev_main0, s));  // moved to the main launch when a check runs in between
+    if (const char *e = dev_knob("PTV_DBG_LATDK")) {  // dev builds: the finest lattice bounds to a file
+        if (nlat > 0) {
+            const size_t np = (size_t)lat[0].n[0] * lat[0].n[1] * lat[0].n[2];
+            std::vector<double> h(np);
+            PTV_HIP(hipMemcpyAsync(h.data(), lat[0].dk, np * sizeof(double), hipMemcpyDeviceToHost, s));
+            PTV_HIP(hipStreamSynchronize(s));
+            if (FILE *f = std::fopen(e, "wb")) {
+                std::fwrite(lat[0].n, sizeof(int), 3, f);
+                std::fwrite(h.data(), sizeof(double), np, f);
+                std::fclose(f);
+            }
+        }
+    }
 
     ptv_stats &ls = c->last;
     ls = ptv_stats{};
@@ -709,6 +746,9 @@ int run_knn_auto(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const pt
     // bitwise comparison (a NaN fingerprint value never matches itself otherwise)
     bool use_map = c->cmap_valid && c->ckey.size() == key.size() &&
                    std::memcmp(c->ckey.data(), key.data(), key.size() * sizeof(double)) == 0;
+    if (dev_knob("PTV_DBG_CULL"))
+        std::fprintf(stderr, "[cull] slab [%lld, %lld) n %lld: cached map %d, key match %d\n", (long long)g->z_begin,
+                     (long long)g->z_end, (long long)n, (int)c->cmap_valid, (int)use_map);
     for (int attempt = 0; attempt < 2; ++attempt) {
         KnnLaunch kl;
         Binned b{};
@@ -746,13 +786,14 @@ int run_knn_auto(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const pt
                 c->cull_timed = true;
             }
         }
-        PTV_TRY(prepare(c, &pe, g, &sp, ax, ay, az, nullptr, nullptr, nullptr, s, kl, b, culled ? c->h_bbox : nullptr));
+        PTV_TRY(prepare(c, &pe, g, &sp, ax, ay, az, nullptr, nullptr, nullptr, s, kl, b, culled ? c->h_bbox : nullptr,
+                        true));
         if (kl.cb.dk == nullptr) {
             // no lattice bounds (nothing to prove the cull or to build a map from): every particle
             if (culled) {
                 culled = false;
                 c->cull_timed = false;
-                PTV_TRY(prepare(c, p, g, &sp, ax, ay, az, nullptr, nullptr, nullptr, s, kl, b));
+                PTV_TRY(prepare(c, p, g, &sp, ax, ay, az, nullptr, nullptr, nullptr, s, kl, b, nullptr, true));
             }
             PTV_TRY(launch_knn(kl, b, ax, ay, az, nullptr, nullptr, nullptr, mask, U, V, W, s));
             PTV_HIP(hipEventRecord(c->ev_knn1, s));
@@ -794,8 +835,8 @@ int run_knn_auto(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const pt
             CullMap used = geo;
             used.top = c->cmap[0].p;
             used.bot = c->cmap[1].p;
-            PTV_TRY(launch_cull_need(kl.cb.ax, kl.cb.ay, kl.cb.az, kl.cb.n, kl.cb.dk, kl.cg.mg, geo, c->cneed[0].p,
-                                     c->cneed[1].p, c->ccols.p, c->ckeys.p, &used, c->halo_need.p, s));
+            PTV_TRY(launch_cull_need(kl.cb.ax, kl.cb.ay, kl.cb.az, kl.cb.n, kl.cb.dk, kl.cg.mg, 0.0, geo,
+                                     c->cneed[0].p, c->cneed[1].p, c->ccols.p, c->ckeys.p, &used, c->halo_need.p, s));
             kl.gate = c->halo_need.p;
             kl.gate_halo = 0.0;
             PTV_HIP(hipEventRecord(c->ev_main0, s));
@@ -808,8 +849,10 @@ int run_knn_auto(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const pt
         if (!culled) {
             // every particle binned: this call's lattice gives the map later calls cull with
             for (auto &d : c->cmap) PTV_TRY(d.ensure(nm));
-            PTV_TRY(launch_cull_need(kl.cb.ax, kl.cb.ay, kl.cb.az, kl.cb.n, kl.cb.dk, kl.cg.mg, geo, c->cmap[0].p,
-                                     c->cmap[1].p, c->ccols.p, c->ckeys.p, nullptr, nullptr, s));
+            // (widened by kCullMapSlack: the packed-key lattice bounds of a culled call carry other slots in
+            // their low bits, a few 1e-9 relative from this call's)
+            PTV_TRY(launch_cull_need(kl.cb.ax, kl.cb.ay, kl.cb.az, kl.cb.n, kl.cb.dk, kl.cg.mg, kCullMapSlack, geo,
+                                     c->cmap[0].p, c->cmap[1].p, c->ccols.p, c->ckeys.p, nullptr, nullptr, s));
             c->cmap_geo = geo;
             c->cmap_valid = true;
             c->ckey = key;
@@ -818,6 +861,23 @@ int run_knn_auto(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const pt
         }
         PTV_HIP(hipMemcpyAsync(c->h_misc + 1, c->halo_need.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
         PTV_HIP(hipStreamSynchronize(s));
+        if (dev_knob("PTV_DBG_CULL")) {  // dev builds: the map, the need and the proof
+            std::vector<double> t(nm), b2(nm), nt(nm), nb2(nm);
+            PTV_HIP(hipMemcpy(t.data(), c->cmap[0].p, nm * sizeof(double), hipMemcpyDeviceToHost));
+            PTV_HIP(hipMemcpy(b2.data(), c->cmap[1].p, nm * sizeof(double), hipMemcpyDeviceToHost));
+            PTV_HIP(hipMemcpy(nt.data(), c->cneed[0].p, nm * sizeof(double), hipMemcpyDeviceToHost));
+            PTV_HIP(hipMemcpy(nb2.data(), c->cneed[1].p, nm * sizeof(double), hipMemcpyDeviceToHost));
+            int over = 0;
+            for (size_t i = 0; i < nm; ++i) over += (nt[i] > t[i] || nb2[i] < b2[i]) ? 1 : 0;
+            std::fprintf(stderr, "[cull] slab [%lld, %lld) kept %lld of %lld, map %dx%d, top [%g, %g] bot [%g, %g], "
+                                 "need top [%g, %g] bot [%g, %g], cells short %d, proof %llx\n",
+                         (long long)g->z_begin, (long long)g->z_end, (long long)pe.n, (long long)n, geo.mx, geo.my,
+                         *std::min_element(t.begin(), t.end()), *std::max_element(t.begin(), t.end()),
+                         *std::min_element(b2.begin(), b2.end()), *std::max_element(b2.begin(), b2.end()),
+                         *std::min_element(nt.begin(), nt.end()), *std::max_element(nt.begin(), nt.end()),
+                         *std::min_element(nb2.begin(), nb2.end()), *std::max_element(nb2.begin(), nb2.end()), over,
+                         (unsigned long long)c->h_misc[1]);
+        }
         if (c->h_misc[1] == 0ull) {  // proven: the gated launch wrote every output
             c->last.halo_required = 0.0;
             if (st) *st = c->last;

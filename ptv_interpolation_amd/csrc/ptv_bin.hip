@@ -483,7 +483,7 @@ constexpr int kColFields = 7;  // x lo, x hi, y lo, y hi, T, B, Rm
 
 __global__ __launch_bounds__(256) void k_cull_columns(const double *__restrict__ lax, const double *__restrict__ lay,
                                                       const double *__restrict__ laz, int n0, int n1, int n2,
-                                                      const double *__restrict__ dk, double mg,
+                                                      const double *__restrict__ dk, double mg, double slack,
                                                       double *__restrict__ cols) {
     const int c0 = max(n0 - 1, 1), c1 = max(n1 - 1, 1), c2 = max(n2 - 1, 1);
     const int t = (int)(blockIdx.x * blockDim.x + threadIdx.x);
@@ -500,7 +500,7 @@ __global__ __launch_bounds__(256) void k_cull_columns(const double *__restrict__
         const double dz = fabs(zb - za);
         const double dmax = fmax(fmax(fmax(D(i, j, l), D(i1, j, l)), fmax(D(i, j1, l), D(i1, j1, l))),
                                  fmax(fmax(D(i, j, l1), D(i1, j, l1)), fmax(D(i, j1, l1), D(i1, j1, l1))));
-        const double U = (dmax + 0.5 * sqrt((dx * dx + dy * dy) + dz * dz)) * (1.0 + 1e-9) + mg;
+        const double U = (dmax + 0.5 * sqrt((dx * dx + dy * dy) + dz * dz)) * (1.0 + 1e-9 + slack) + mg;
         T = fmax(T, fmax(za, zb) + U);
         B = fmin(B, fmin(za, zb) - U);
         Rm = fmax(Rm, U);
@@ -586,12 +586,12 @@ __global__ __launch_bounds__(256) void k_cull_map_final(const unsigned long long
 }
 
 int launch_cull_need(const double *lax, const double *lay, const double *laz, const int n[3], const double *dk,
-                     double mg, const CullMap &m, double *top, double *bot, double *cols, unsigned long long *keys,
-                     const CullMap *used, unsigned long long *fail, hipStream_t s) {
+                     double mg, double slack, const CullMap &m, double *top, double *bot, double *cols,
+                     unsigned long long *keys, const CullMap *used, unsigned long long *fail, hipStream_t s) {
     const int ncol = std::max(n[0] - 1, 1) * std::max(n[1] - 1, 1);
     const int nm = m.mx * m.my;
     hipLaunchKernelGGL(k_cull_columns, dim3((ncol + 255) / 256), dim3(256), 0, s, lax, lay, laz, n[0], n[1], n[2], dk, mg,
-                       cols);
+                       slack, cols);
     hipLaunchKernelGGL(k_cull_map_init, dim3((nm + 255) / 256), dim3(256), 0, s, keys, keys + nm, nm);
     hipLaunchKernelGGL(k_cull_map, dim3((nm + 255) / 256, (ncol + kMapChunk - 1) / kMapChunk), dim3(256), 0, s,
                        (const double *)cols, ncol, m, keys, keys + nm);

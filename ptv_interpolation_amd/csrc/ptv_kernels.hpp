@@ -40,12 +40,13 @@ int launch_cull(const double *const src[6], int64_t n, const double *az, int z0,
                 const CullMap *map = nullptr);
 // the map a slab needs, from its finest lattice (axes lax / lay / laz, n[3] points, k-th distance
 // bounds dk over the particles binned): top / bot per cell of m's geometry; cols: 7 (n0-1)(n1-1)
-// doubles and keys: 2 mx my u64 of scratch.  With `used` (the map the binned particles were
-// culled with) *fail is set to 0 when the need fits inside it everywhere (the cull is proven
-// exact), else to +inf's bits (ptv_knn_params.slab_halo's gate convention).
+// doubles and keys: 2 mx my u64 of scratch; every cell reach U is widened by the relative `slack`.
+// With `used` (the map the binned particles were culled with) *fail is set to 0 when the need fits
+// inside it everywhere (the cull is proven exact), else to +inf's bits (the slab_halo gate's
+// convention).
 int launch_cull_need(const double *lax, const double *lay, const double *laz, const int n[3], const double *dk,
-                     double mg, const CullMap &m, double *top, double *bot, double *cols, unsigned long long *keys,
-                     const CullMap *used, unsigned long long *fail, hipStream_t s);
+                     double mg, double slack, const CullMap &m, double *top, double *bot, double *cols,
+                     unsigned long long *keys, const CullMap *used, unsigned long long *fail, hipStream_t s);
 
 // 6 * kFingerprint doubles identifying a particle set (the cull map cache's key, with n and the arrays)
 constexpr int kFingerprint = 16;

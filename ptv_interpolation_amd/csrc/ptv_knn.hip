@@ -155,7 +155,8 @@ __global__ __launch_bounds__(1024) void k_block_order(const double *__restrict__
                                                       int *__restrict__ order) {
     __shared__ int cnt[256];
     __shared__ int base[256];
-    auto bucket = [&](int b) -> int {
+    __shared__ double dmx[1024];
+    auto key = [&](int b) -> double {
         // block b: tiles (bx*4 .. bx*4+3, ty, tz) = points x [16 bx, 16 bx + 15], y [4 ty, 4 ty + 3],
         // z [4 tz, 4 tz + 3]; coarser point j sits at point 4 j (kLatticeStep), so the block lies in
         // the coarser cells spanned by x [4 bx, 4 bx + 4], y [ty, ty + 1], z [tz, tz + 1]
@@ -165,7 +166,21 @@ __global__ __launch_bounds__(1024) void k_block_order(const double *__restrict__
             for (int y = ty; y <= ty + 1; ++y)
                 for (int x = 4 * bx; x <= 4 * bx + 4; ++x)
                     D = fmax(D, dkc[((size_t)min(z, cnz - 1) * cny + min(y, cny - 1)) * cnx + min(x, cnx - 1)]);
-        const double q = D * inv_unit;
+        return D;
+    };
+    // buckets of the largest key / 256 (a fixed unit saturated: at 512^3 every block near a sphere
+    // centre fell into the top bucket, in arbitrary order, and the slowest void tile could start last)
+    double m = 0.0;
+    for (int b = threadIdx.x; b < nblocks; b += blockDim.x) m = fmax(m, key(b));
+    dmx[threadIdx.x] = m;
+    __syncthreads();
+    for (int st = 512; st > 0; st >>= 1) {
+        if ((int)threadIdx.x < st) dmx[threadIdx.x] = fmax(dmx[threadIdx.x], dmx[threadIdx.x + st]);
+        __syncthreads();
+    }
+    const double scale = dmx[0] > 0.0 && dmx[0] < INFINITY ? 255.99 / dmx[0] : inv_unit;
+    auto bucket = [&](int b) -> int {
+        const double q = key(b) * scale;
         return 255 - (q < 255.0 ? (int)q : 255);  // descending bound -> ascending bucket
     };
     for (int i = threadIdx.x; i < 256; i += blockDim.x) cnt[i] = 0;

@@ -130,7 +130,7 @@ struct KnnKernelArgs {
     double gate_halo;
     // lattice void tiles (kModeKDist, see k_kdist_merge): a split launch runs `split` waves per
     // tile over the first split_tiles tiles of the block order (tile t = block order[t / 4], x-tile
-    // t % 4), wave part p taking every split-th candidate window of one pass at the lattice bound,
+    // t % 4), wave part p taking every split-th cell row of one pass at the lattice bound,
     // and leaves its partial list in split_out[((t * split + p) * KMAX + j) * 64 + lane] (slots,
     // ~0 = none); 0 = an ordinary launch
     int split;
@@ -720,7 +720,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
     if (a.gate != nullptr && !(__longlong_as_double((long long)*a.gate) <= a.gate_halo))
         return;  // slab cull not proven exact: no outputs (the call returns PTV_E_INEXACT)
     int b, tw;  // block of the tile grid, wave (x-tile) within it
-    // split lattice launch: this wave's part of its tile's candidate windows (wave-uniform)
+    // split lattice launch: this wave's part of its tile's cell rows (wave-uniform)
     int part = 0, nparts = 1;
     bool split_epi = false;
     if (MODE == kModeKDist && a.split > 0) {
@@ -1344,15 +1344,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
             const int nyr = 2 * hy + 1;
             const int nrows = nyr * (2 * hz + 1);
             const float inv_nyr = 1.0f / (float)nyr;
-            int wbase = 0;  // candidate windows of this pass's earlier rounds (split launches)
-            for (int rb = 0; rb < nrows; rb += 64 * kRowsPerLane) {
+            // this wave's rows: every one, or (split lattice launch) every nparts-th from its part, still
+            // centre-out.  Each part clips its runs to its own sub-balls: a candidate outside them is
+            // farther from every lane than the part's k-th, which bounds the merged k-th from above
+            const int nrp = (nrows - part + nparts - 1) / nparts;
+            for (int rb = 0; rb < nrp; rb += 64 * kRowsPerLane) {
                 ++n_round;
                 // ---- lane = kRowsPerLane cell rows: x-runs of this shell -> particle ranges ----
                 uint32_t rs[2 * kRowsPerLane];
                 int rc[2 * kRowsPerLane];
 #pragma unroll
                 for (int q = 0; q < kRowsPerLane; ++q) {
-                    const int row = rb + q * 64 + lane;
+                    const int row = part + nparts * (rb + q * 64 + lane);
                     rs[2 * q] = rs[2 * q + 1] = 0;
                     rc[2 * q] = rc[2 * q + 1] = 0;
                     if (row < nrows) {
@@ -1466,22 +1469,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                     }
                     return sl;
                 };
-                // this wave's windows: every one, or (split launch) those whose index within the
-                // pass is congruent to its part modulo the parts
-                const int wstride = 64 * nparts;
-                const int src0 = 64 * ((part - wbase % nparts + nparts) % nparts);
-                wbase += (total + 63) >> 6;
-                uint32_t next_slot = src0 < total ? window_slot(src0) : 0u;
+                uint32_t next_slot = total > 0 ? window_slot(0) : 0u;
                 double4 next_rec = prec[next_slot];
                 // the pass's last round runs at least one (possibly empty) window, so that the
                 // final flush below is the loop's own (one inlined copy of the insert network)
-                const bool last_round = rb + 64 * kRowsPerLane >= nrows;
-                const int tot_it = last_round ? max(total, src0 + 1) : total;
-                for (int src = src0; src < tot_it; src += wstride) {
+                const bool last_round = rb + 64 * kRowsPerLane >= nrp;
+                const int tot_it = (total == 0 && last_round) ? 1 : total;
+                for (int src = 0; src < tot_it; src += 64) {
                     const uint32_t slot = next_slot;
                     const double4 p4 = next_rec;
-                    if (src + wstride < total) {
-                        next_slot = window_slot(src + wstride);
+                    if (src + 64 < total) {
+                        next_slot = window_slot(src + 64);
                         next_rec = prec[next_slot];
                     }
                     const int i = src + lane;
@@ -1514,9 +1512,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                         fbz[pos] = ez;
                     }
                     nbuf += __builtin_popcountll(km);
-                    n_cand += (uint32_t)max(0, min(64, total - src));
+                    n_cand += (uint32_t)min(64, total - src);
                     stamp(t_copy);
-                    if (nbuf > kCap - 64 || (last_round && src + wstride >= tot_it)) flush();
+                    if (nbuf > kCap - 64 || (last_round && src + 64 >= tot_it)) flush();
                 }
             }
             // ---- exactness: lanes with k-th distance <= R are final ----
@@ -2296,7 +2294,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
 // the particle shell around it (~59k candidates at 512^3 / 5M) in one wave: 1.7 of the 1.8 ms
 // lattice level, on the critical path of every launch and z-slab that holds it.  The launcher runs
 // the first tiles of the longest-first block order as a split launch (KnnKernelArgs::split: S
-// waves per tile, each taking every S-th candidate window of one pass at the lattice bound, which
+// waves per tile, each taking every S-th cell row of one pass at the lattice bound, which
 // covers every lane's k nearest) and merges the S partial lists here: one wave per tile, lane =
 // lattice point, each listed slot's exact d2 recomputed (bit-identical to the search's) and
 // inserted into a fresh list.  The k smallest of the union are the k smallest of the parts' k

@@ -31,3 +31,10 @@ run filter 300 --method filter
 run mask 300 --method mask
 run div_f64 300 --method div
 run div_f32 300 --method div --div-dtype f32
+# one-GPU rehearsal of every rank share of the strong split (only when LINES names them)
+for s in 0/8 1/8 2/8 3/8 4/8 5/8 6/8 7/8 0/4 1/4 2/4 3/4 0/2 1/2; do
+  n=share_${s/\//of}
+  if [ -n "$LINES" ] && [[ " $LINES " == *" $n "* || " $LINES " == *" shares "* ]]; then
+    LINES="$n" run $n 300 --share $s --no-cpu-baseline
+  fi
+done

@@ -3,9 +3,9 @@
 # kernel-trace stats and the FETCH_SIZE / WRITE_SIZE passes of the default bench command (turned
 # into profiles/traffic_<tag>.json on the box, so that every bench line after it carries the
 # measured traffic of this very build), then every bench line (tools/gpu_lines.sh).
-# usage: gpurun -- bash tools/gpu_r04_final.sh r04
+# usage: gpurun -- bash tools/gpu_round_final.sh r05
 set -o pipefail
-tag=${1:-r04}
+tag=${1:-r05}
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 mkdir -p gpurun_out
 if [ -z "$SKIP_TESTS" ]; then
