@@ -120,14 +120,13 @@ def rbf_resolved(args):
 def rbf_kernel_label(kern, k, m, deg):
     """The solver launch_rbf (ptv_rbf.hip) picks: k_rbf_spd16 for the SPD kernels without a
     polynomial (M <= 32), the null-space k_rbf_ns for the scale-invariant kernels with degree >= their
-    minimum (1, 4 or 10 monomials, k <= 32; 10 only for k <= 24), else the pivoting k_rbf_local."""
+    minimum and 1 or 4 monomials (k <= 32), else the pivoting k_rbf_local."""
     M = (m + 7) & ~7
     npoly = m - k
     if kern in ("gaussian", "inverse_multiquadric", "inverse_quadratic") and m == k and M <= 32:
         return f"k_rbf_spd16<{M}>"
     min_deg = {"linear": 0, "thin_plate_spline": 1, "cubic": 1, "quintic": 2}
-    if (kern in min_deg and deg >= min_deg[kern] and npoly in (1, 4, 10) and npoly < k <= 32
-            and (npoly < 10 or k <= 24)):
+    if kern in min_deg and deg >= min_deg[kern] and npoly in (1, 4) and npoly < k <= 32:
         nc = 16 if k <= 16 else 20 if k <= 20 else 24 if k <= 24 else 32
         return f"k_rbf_ns<{nc}, {npoly}>"
     return f"k_rbf_local<{M}>" if M <= 64 else "k_rbf_big"

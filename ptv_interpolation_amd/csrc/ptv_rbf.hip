@@ -1127,16 +1127,23 @@ static bool rbf_spd(const RbfKernelArgs &ka, const double *smooth) {
 
 // whether k_rbf_ns (ptv_rbf_ns.hpp) serves the launch: a scale-invariant conditionally positive
 // definite kernel (the kernels interpolate_field can reach, interpolator.py:162-167: no epsilon
-// there) with degree >= its order - 1 (then (Q^T Phi Q)[r:, r:] is positive definite), 1, 4 or
-// 10 monomials, k <= 32 row slots (10 monomials: k <= 24, registers).  The scale-dependent
-// kernels stay on the pivoting kernel: for the flat gaussian eps = 0.3 systems (cond 6e8) the
-// projected system lost 20x LAPACK's accuracy (tools/rbf_nullspace_proto.py).
+// there) with degree >= its order - 1 (then (Q^T Phi Q)[r:, r:] is positive definite), 1 or 4
+// monomials, k <= 32 row slots.  The scale-dependent kernels stay on the pivoting kernel: for the
+// flat gaussian eps = 0.3 systems (cond 6e8) the projected system lost 20x LAPACK's accuracy
+// (tools/rbf_nullspace_proto.py).  So do 10 monomials (degree 2, the quintic's minimum): on the
+// sphere pack's void voxels (neighbourhoods on a sphere-shell cap, a nearly degenerate quadratic
+// fit) the null-space solve landed 1.2e-10 from the exact answer against LAPACK's 8.7e-13
+// (tests/test_gpu_rbf.py::test_nullspace_sphere_pack_sampled, round 5); the dev knob
+// PTV_RBF_NS=10 re-enables it.
 static bool rbf_ns(const RbfKernelArgs &ka, const double *smooth, long long nvox) {
     if (const char *e = dev_knob("PTV_RBF_NS"))  // dev knob: 0 = the pivoting kernel throughout
         if (e[0] == '0') return false;
     if (ka.ns_list == nullptr || ka.ns_cap <= 0 || nvox > 0xffffffffLL || (ka.flags & PTV_FLAG_RBF_PIVOTING)) return false;
     const int np = ka.m - ka.k;
-    if (!(np == 1 || np == 4 || (np == 10 && ka.k <= 24))) return false;
+    bool ns10 = false;
+    if (const char *e = dev_knob("PTV_RBF_NS"))
+        ns10 = std::atoi(e) == 10;
+    if (!(np == 1 || np == 4 || (ns10 && np == 10 && ka.k <= 24))) return false;
     if (ka.k <= np || ka.k > 32) return false;
     // scalar smoothing the kernel would flag on every voxel (negative, or > 2^26: k_rbf_ns step 1)
     if (smooth == nullptr && !(ka.smoothing >= 0.0 && ka.smoothing <= 0x1p26)) return false;
