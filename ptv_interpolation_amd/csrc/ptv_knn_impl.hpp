@@ -85,6 +85,12 @@ namespace ptv {
 #endif
 
 constexpr int kStampFields = 8;
+#ifndef PTV_TIGHTEN_MIN
+#define PTV_TIGHTEN_MIN 32
+#endif
+// lattice levels: insertions per group that pay for the fp32 k-th network (same-box A/B, 512^3 / 5M:
+// lattice 1.86 ms without it, 1.80 at 16, 1.72 at 32; C2 and the 2/8 share unchanged)
+constexpr int kTightenMin = PTV_TIGHTEN_MIN;
 constexpr int kCap = 128;        // LDS candidate slots per wave (16 B fp32 + 32 B fp64 each)
 constexpr int kRowsPerLane = 1;  // cell rows examined per lane per gather round
 constexpr int kRunEntries = 64 * 2 * kRowsPerLane;  // x-runs per gather round (power of two)
@@ -1237,8 +1243,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
             for (int g0 = 0; g0 < nbuf; g0 += 64) {
                 const int ng = min(64, nbuf - g0);
                 // candidate g0 + j ends at bit nb - 1 - j (shift-in order keeps the loop rolled)
-                unsigned long long m = 0ull;
                 const int nb = (ng + 3) & ~3;
+                auto group_mask = [&]() -> unsigned long long {
+                unsigned long long m = 0ull;
 #pragma unroll 1
                 for (int i0 = 0; i0 < ng; i0 += 4) {
                     // 4 candidates as two packed-fp32 pairs (v_pk_add / v_pk_mul / v_pk_fma);
@@ -1258,9 +1265,51 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                                         ((s1.x <= thrf) ? 2u : 0u) | ((s1.y <= thrf) ? 1u : 0u);
                     m = (m << 4) | b4;
                 }
-                m &= ~((1ull << (nb - ng)) - 1ull);  // stale slots past nbuf
+                return m & ~((1ull << (nb - ng)) - 1ull);  // stale slots past nbuf
+                };
+                unsigned long long m = group_mask();
                 const double4 *gbuf = buf + g0 + nb - 64;  // bit position p <-> gbuf[63 - p]
-                const int nit = __builtin_amdgcn_readfirstlane(wave_max_i(__builtin_popcountll(m)));
+                int nit = __builtin_amdgcn_readfirstlane(wave_max_i(__builtin_popcountll(m)));
+                if constexpr (MODE == kModeKDist && !KEYS) {
+                    // lattice levels start from the coarse bound (no seeds): a lane whose list is not
+                    // full yet takes every candidate under it.  When some lane would insert more than
+                    // kTightenMin of this group, first each lane's k-th smallest fp32 d2 over its list
+                    // and the group (fmed3 network; list entries rounded up, the group's within cpass):
+                    // an upper bound on the k-th of the two, so the insertions keep to the candidates
+                    // that can stay in the list (the lists come out the same)
+                    if (nit > kTightenMin) {
+                        float sd[KMAX];
+#pragma unroll
+                        for (int j = 0; j < KMAX; ++j)
+                            sd[j] = bd[j] < 0.0 ? -1.0f
+                                                : (bd[j] < INFINITY ? (float)(bd[j] * (1.0 + 2.384185791015625e-07)) : INFINITY);
+                        for (int i = 0; i < ng; i += 2) {
+                            const float2 X = *reinterpret_cast<const float2 *>(fbx + g0 + i);
+                            const float2 Y = *reinterpret_cast<const float2 *>(fby + g0 + i);
+                            const float2 Z = *reinterpret_cast<const float2 *>(fbz + g0 + i);
+                            const f32x2 ex = qf2x - f32x2{X.x, X.y}, ey = qf2y - f32x2{Y.x, Y.y}, ez = qf2z - f32x2{Z.x, Z.y};
+                            f32x2 s2 = ex * ex;
+                            s2 = __builtin_elementwise_fma(ey, ey, s2);
+                            s2 = __builtin_elementwise_fma(ez, ez, s2);
+                            const float xs[2] = {s2.x, i + 1 < ng ? s2.y : INFINITY};
+#pragma unroll
+                            for (int u = 0; u < 2; ++u) {
+#pragma unroll
+                                for (int q = KMAX - 1; q > 0; --q) sd[q] = __builtin_amdgcn_fmed3f(sd[q - 1], sd[q], xs[u]);
+                                sd[0] = fminf(sd[0], xs[u]);
+                            }
+                        }
+                        if (active && sd[KMAX - 1] >= 0.0f && sd[KMAX - 1] < INFINITY) {
+                            const double t = ((double)sd[KMAX - 1] * (1.0 + 9.5367431640625e-07) + cpass) * (1.0 + 1e-12);
+                            if (t < thr) {
+                                thr = t;
+                                thrf = f32_bound(thr, cpass);
+                            }
+                        }
+                        m = group_mask();
+                        nit = __builtin_amdgcn_readfirstlane(wave_max_i(__builtin_popcountll(m)));
+                    }
+                }
                 if constexpr (KEYS && MODE != kModeRadius) {
                     // key lists: NB candidates per lane at a time into one merge network
                     // (insert_keys); iterations past nit find m = 0 everywhere (+inf keys).
