@@ -169,6 +169,11 @@ def parse():
                          "are skipped and written as 0")
     ap.add_argument("--div", action="store_true", default=None,
                     help="k-NN methods: + consistent divergence of each slab (C5)")
+    ap.add_argument("--slabs", default=None, metavar="b0,b1,...,bN",
+                    help="strong scaling: explicit z-slab plane boundaries (N + 1 of them) instead of the even cut")
+    ap.add_argument("--no-balance", action="store_true",
+                    help="N>1: keep the even (or --slabs) cut; default: re-cut the slabs during the warmup from the "
+                         "ranks' measured step times (zslab.balanced_bounds), fixed before the timed steps")
     ap.add_argument("--halo", type=float, default=None,
                     help="N>1: the scalar slab_halo cull starting at this halo (zslab.interp_slab retries) instead "
                          "of the per-column map (PTV_FLAG_SLAB_CULL_AUTO, default)")
@@ -575,7 +580,14 @@ def main_interp(args):
     if args.method == "nearest":
         k = args.k = 1
     nz = G * world if weak else G
-    z0, z1 = (rank * G, (rank + 1) * G) if weak else zslab.rank_slab(G, world, rank)
+    if args.slabs:
+        bounds = [int(v) for v in args.slabs.split(",")]
+        if weak or len(bounds) != world + 1 or bounds[0] != 0 or bounds[-1] != nz or \
+                any(bounds[i] >= bounds[i + 1] for i in range(world)):
+            raise SystemExit(f"bench.py: --slabs needs {world + 1} increasing boundaries from 0 to {nz}")
+    else:
+        bounds = [0] + [zslab.rank_slab(nz, world, r)[1] for r in range(world)] if not weak else None
+    z0, z1 = (rank * G, (rank + 1) * G) if weak else (bounds[rank], bounds[rank + 1])
     za, zb, hlo, hhi = zslab.halo_slab(z0, z1, nz, 1 if args.div else 0)
 
     # particles: replicated on every rank (north_star); weak: copy r generated by rank r and
@@ -642,8 +654,39 @@ def main_interp(args):
                                div_out.data_ptr(), 1.0, 1.0, 1.0, field_dtype=dtc, result_dtype=dtc,
                                z_range=(hlo, hlo + (z1 - z0)), edges=(hlo == 0, hhi == 0), stream=stream)
 
-    for _ in range(args.warmup):
+    # load balance (N > 1, strong k-NN configs): the sphere pack's void planes cost more per plane
+    # than its packed ones, so the even cut leaves the void-heavy slabs last.  After warmup steps 1
+    # and 3 every rank's device time of its step is all-gathered and the slabs are re-cut
+    # (zslab.balanced_bounds); the next warmup step builds the new slab's cull map, and the cut is
+    # fixed before the timed steps (the same grid, the same particles: strong scaling unchanged)
+    balance = (dist is not None and world > 1 and not weak and not rbf and not args.div and not args.no_balance
+               and not args.slabs)
+    rebalances = []
+
+    def rebalance():
+        nonlocal z0, z1, za, zb, out, optrs, bounds, mask_t, fluid_frac
+        st = ctx.last_stats()
+        t = torch.tensor([st["ms_bin"] + st["ms_cull"] + st["ms_lattice"] + st["ms_knn"]], dtype=torch.float64,
+                         device=dev)
+        ts = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(ts, t)
+        times = [float(x.item()) for x in ts]
+        new = zslab.balanced_bounds(bounds, times)
+        rebalances.append({"bounds": bounds, "ms": [round(v, 3) for v in times]})
+        if new != bounds:
+            bounds = new
+            z0, z1 = bounds[rank], bounds[rank + 1]
+            za, zb = z0, z1
+            out = [torch.empty((zb - za, G, G), dtype=odt, device=dev) for _ in range(3)]
+            optrs = [o.data_ptr() for o in out]
+            if mask_t is not None:
+                mask_t = _device_fluid_mask(G, nz, (za, zb), dev)
+                fluid_frac = float(mask_t[z0:z1].float().mean().item())
+
+    for w in range(args.warmup):
         step()
+        if balance and w in (1, 3) and w + 1 < args.warmup:
+            rebalance()
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
@@ -670,7 +713,7 @@ def main_interp(args):
     # RCCL all-gather reassembly of the full field, once, reported apart from `value`
     gather_ms = None
     if dist is not None and not args.no_allgather:
-        counts = [b - a for a, b in (((r * G, (r + 1) * G) if weak else zslab.rank_slab(nz, world, r))
+        counts = [b - a for a, b in (((r * G, (r + 1) * G) if weak else (bounds[r], bounds[r + 1]))
                                      for r in range(world))]
         try:
             for it in range(2):  # the first all-gather sets RCCL's channels up: time the second
@@ -790,6 +833,11 @@ def main_interp(args):
             line["share"] = {"rank": rank, "world": world}
         if args.mask:
             line["fluid_mvoxels_per_s"] = round(value * fluid_frac, 2)
+        if bounds is not None and world > 1:
+            line["slabs"] = {"bounds": bounds, "rebalances": rebalances,
+                             "how": ("re-cut from the ranks' measured step times during the warmup "
+                                     "(zslab.balanced_bounds)" if balance else
+                                     ("explicit --slabs" if args.slabs else "even cut"))}
         if cull:
             line["cull"] = ({"mode": "scalar slab_halo", **halo.as_dict()} if halo is not None else
                             {"mode": "per-column map (PTV_FLAG_SLAB_CULL_AUTO), proven on the device"})
@@ -1193,6 +1241,23 @@ def main_dryrun(args):
     digests = [torch.empty_like(digest) for _ in range(world)] if dist else [digest]
     if dist:
         dist.all_gather(digests, digest)
+    # the warmup re-cut of the GPU path (zslab.balanced_bounds over all-gathered step times), with a
+    # synthetic cost of 1 per plane plus 2 per plane in the middle third standing in for the kernel's
+    bounds = [0] + [zslab.rank_slab(nz, world, r)[1] for r in range(world)]
+    cost = lambda a, b: float(sum(1.0 + (2.0 if nz // 3 <= z < 2 * nz // 3 else 0.0) for z in range(a, b)))  # noqa: E731
+    spread = []
+    for _ in range(2):
+        t = torch.tensor([cost(bounds[rank], bounds[rank + 1])], dtype=torch.float64)
+        ts = [torch.zeros_like(t) for _ in range(world)] if dist else [t]
+        if dist:
+            dist.all_gather(ts, t)
+        times = [float(x.item()) for x in ts]
+        spread.append(max(times) / min(times))
+        bounds = zslab.balanced_bounds(bounds, times, min_planes=1)
+    bt = torch.tensor(bounds, dtype=torch.float64)
+    allb = [torch.zeros_like(bt) for _ in range(world)] if dist else [bt]
+    if dist:
+        dist.all_gather(allb, bt)
     if rank == 0:
         ok = (tuple(full.shape) == (nz, G, G) and
               bool(torch.equal(full[:, 0, 0], torch.arange(nz, dtype=torch.float64))) and
@@ -1201,7 +1266,9 @@ def main_dryrun(args):
                           "gpus_flag": args.gpus, "grid": G, "particles": args.particles,
                           "partition": [list(zslab.rank_slab(nz, world, r)) for r in range(world)],
                           "particles_agree": len({float(d.item()) for d in digests}) == 1,
-                          "field_reassembled": ok}), flush=True)
+                          "field_reassembled": ok,
+                          "balanced": {"bounds": bounds, "ranks_agree": all(torch.equal(x, bt) for x in allb),
+                                       "cost_spread": [round(v, 4) for v in spread]}}), flush=True)
     if dist:
         dist.barrier()
         dist.destroy_process_group()

@@ -77,9 +77,10 @@ struct ptv_ctx {
     DevBuf<uint32_t> lat_split;                                  // split lattice launch: partial lists
     // PTV_FLAG_SLAB_CULL_AUTO: the cached per-column cull map (top, bot), its key, the proof's
     // need map and scratch
-    DevBuf<double> cmap[2], cneed[2], ccols, cfp;
+    DevBuf<double> cmap[2], cdk, ccols, cfp;  // map (top, bot), the lattice bounds it came from, scratch
     DevBuf<unsigned long long> ckeys;
     CullMap cmap_geo{};
+    int cdk_n[3] = {0, 0, 0};
     bool cmap_valid = false;
     std::vector<double> ckey, ckey_new;
     DevBuf<uint32_t> slots;                                      // local RBF: chunk k-NN slots
@@ -98,6 +99,7 @@ struct ptv_ctx {
     DevBuf<double> flt_kth, flt_spd;
     DevBuf<double> cull[6], cull_win;                            // slab cull: kept particles, z window
     DevBuf<uint32_t> cull_cnt;                                   // slab cull: per-block counts
+    DevBuf<unsigned long long> cull_mask;                        // slab cull: keep masks (pass 1 -> pass 2)
     DevBuf<unsigned long long> halo_need;                        // slab cull: proven halo (double bits)
     DevBuf<unsigned int> rep_cnt;                                // key-list near-tie repair: count
     DevBuf<uint32_t> rep_list;                                   //   and the listed tiles
@@ -229,7 +231,7 @@ int ptv_free(ptv_ctx *c) {
     for (auto &b : c->lat_order) b.release();
     c->lat_split.release();
     for (auto &b : c->cmap) b.release();
-    for (auto &b : c->cneed) b.release();
+    c->cdk.release();
     c->ccols.release();
     c->cfp.release();
     c->ckeys.release();
@@ -260,6 +262,7 @@ int ptv_free(ptv_ctx *c) {
     for (auto &b : c->cull) b.release();
     c->cull_win.release();
     c->cull_cnt.release();
+    c->cull_mask.release();
     c->halo_need.release();
     c->rep_cnt.release();
     c->rep_list.release();
@@ -760,6 +763,7 @@ int run_knn_auto(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const pt
             for (auto &d : c->cull) PTV_TRY(d.ensure(n));
             PTV_TRY(c->cull_win.ensure(4));
             PTV_TRY(c->cull_cnt.ensure(nb + 1));
+            PTV_TRY(c->cull_mask.ensure(cull_mask_words(n)));
             double *dst[6];
             for (int a = 0; a < 6; ++a) dst[a] = c->cull[a].p;
             CullMap used = c->cmap_geo;
@@ -767,8 +771,8 @@ int run_knn_auto(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const pt
             used.bot = c->cmap[1].p;
             uint32_t *h_total = reinterpret_cast<uint32_t *>(c->h_misc);
             PTV_HIP(hipEventRecord(c->ev_cull0, s));
-            PTV_TRY(launch_cull(src, n, az, (int)g->z_begin, (int)g->z_end, 0.0, c->cull_win.p, c->cull_cnt.p, dst,
-                                nullptr, s, &used));
+            PTV_TRY(launch_cull(src, n, az, (int)g->z_begin, (int)g->z_end, 0.0, c->cull_win.p, c->cull_cnt.p,
+                                c->cull_mask.p, dst, nullptr, s, &used));
             PTV_TRY(c->bbox_part.ensure(6 * 1024));
             PTV_TRY(c->bbox_out.ensure(8));
             const double *kp[3] = {dst[0], dst[1], dst[2]};
@@ -829,14 +833,19 @@ int run_knn_auto(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const pt
         PTV_TRY(c->ccols.ensure(7 * ncol));
         PTV_TRY(c->ckeys.ensure(2 * nm));
         PTV_TRY(c->halo_need.ensure(1));
-        if (culled) {
-            // the proof, gating the main launch: the kept particles' lattice needs no more than the map
-            for (auto &d : c->cneed) PTV_TRY(d.ensure(nm));
-            CullMap used = geo;
-            used.top = c->cmap[0].p;
-            used.bot = c->cmap[1].p;
-            PTV_TRY(launch_cull_need(kl.cb.ax, kl.cb.ay, kl.cb.az, kl.cb.n, kl.cb.dk, kl.cg.mg, 0.0, geo,
-                                     c->cneed[0].p, c->cneed[1].p, c->ccols.p, c->ckeys.p, &used, c->halo_need.p, s));
+        const long long nlp = (long long)kl.cb.n[0] * kl.cb.n[1] * kl.cb.n[2];
+        if (culled && !(kl.cb.n[0] == c->cdk_n[0] && kl.cb.n[1] == c->cdk_n[1] && kl.cb.n[2] == c->cdk_n[2])) {
+            // (cannot happen for one key: the lattice follows the grid and the slab) a different
+            // lattice proves nothing against the cached bounds: a failing gate, rerun below
+            PTV_HIP(hipMemsetAsync(c->halo_need.p, 0xff, sizeof(unsigned long long), s));
+            kl.gate = c->halo_need.p;
+            kl.gate_halo = 0.0;
+        } else if (culled) {
+            // the proof, gating the main launch: the need map grows with the lattice bounds, and the
+            // cached map was built from the bounds of the call that binned every particle (widened by
+            // kCullMapSlack), so bounds of the kept particles within half that of the cached ones
+            // prove that the map holds every particle a slab voxel can need
+            PTV_TRY(launch_bounds_within(kl.cb.dk, c->cdk.p, nlp, 1.0 + 0.5 * kCullMapSlack, c->halo_need.p, s));
             kl.gate = c->halo_need.p;
             kl.gate_halo = 0.0;
             PTV_HIP(hipEventRecord(c->ev_main0, s));
@@ -853,6 +862,9 @@ int run_knn_auto(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const pt
             // their low bits, a few 1e-9 relative from this call's)
             PTV_TRY(launch_cull_need(kl.cb.ax, kl.cb.ay, kl.cb.az, kl.cb.n, kl.cb.dk, kl.cg.mg, kCullMapSlack, geo,
                                      c->cmap[0].p, c->cmap[1].p, c->ccols.p, c->ckeys.p, nullptr, nullptr, s));
+            PTV_TRY(c->cdk.ensure((size_t)nlp));
+            PTV_HIP(hipMemcpyAsync(c->cdk.p, kl.cb.dk, (size_t)nlp * sizeof(double), hipMemcpyDeviceToDevice, s));
+            for (int d = 0; d < 3; ++d) c->cdk_n[d] = kl.cb.n[d];
             c->cmap_geo = geo;
             c->cmap_valid = true;
             c->ckey = key;
@@ -861,23 +873,10 @@ int run_knn_auto(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const pt
         }
         PTV_HIP(hipMemcpyAsync(c->h_misc + 1, c->halo_need.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
         PTV_HIP(hipStreamSynchronize(s));
-        if (dev_knob("PTV_DBG_CULL")) {  // dev builds: the map, the need and the proof
-            std::vector<double> t(nm), b2(nm), nt(nm), nb2(nm);
-            PTV_HIP(hipMemcpy(t.data(), c->cmap[0].p, nm * sizeof(double), hipMemcpyDeviceToHost));
-            PTV_HIP(hipMemcpy(b2.data(), c->cmap[1].p, nm * sizeof(double), hipMemcpyDeviceToHost));
-            PTV_HIP(hipMemcpy(nt.data(), c->cneed[0].p, nm * sizeof(double), hipMemcpyDeviceToHost));
-            PTV_HIP(hipMemcpy(nb2.data(), c->cneed[1].p, nm * sizeof(double), hipMemcpyDeviceToHost));
-            int over = 0;
-            for (size_t i = 0; i < nm; ++i) over += (nt[i] > t[i] || nb2[i] < b2[i]) ? 1 : 0;
-            std::fprintf(stderr, "[cull] slab [%lld, %lld) kept %lld of %lld, map %dx%d, top [%g, %g] bot [%g, %g], "
-                                 "need top [%g, %g] bot [%g, %g], cells short %d, proof %llx\n",
+        if (dev_knob("PTV_DBG_CULL"))  // dev builds: the cull and its proof
+            std::fprintf(stderr, "[cull] slab [%lld, %lld) kept %lld of %lld, map %dx%d, proof %llx\n",
                          (long long)g->z_begin, (long long)g->z_end, (long long)pe.n, (long long)n, geo.mx, geo.my,
-                         *std::min_element(t.begin(), t.end()), *std::max_element(t.begin(), t.end()),
-                         *std::min_element(b2.begin(), b2.end()), *std::max_element(b2.begin(), b2.end()),
-                         *std::min_element(nt.begin(), nt.end()), *std::max_element(nt.begin(), nt.end()),
-                         *std::min_element(nb2.begin(), nb2.end()), *std::max_element(nb2.begin(), nb2.end()), over,
                          (unsigned long long)c->h_misc[1]);
-        }
         if (c->h_misc[1] == 0ull) {  // proven: the gated launch wrote every output
             c->last.halo_required = 0.0;
             if (st) *st = c->last;
@@ -917,13 +916,14 @@ int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn
         for (auto &d : c->cull) PTV_TRY(d.ensure(n));
         PTV_TRY(c->cull_win.ensure(4));
         PTV_TRY(c->cull_cnt.ensure(nb + 1));
+        PTV_TRY(c->cull_mask.ensure(cull_mask_words(n)));
         const double *src[6] = {p->x, p->y, p->z, p->u, p->v, p->w};
         double *dst[6];
         for (int a = 0; a < 6; ++a) dst[a] = c->cull[a].p;
         uint32_t *h_total = reinterpret_cast<uint32_t *>(c->h_misc);
         PTV_HIP(hipEventRecord(c->ev_cull0, s));
         PTV_TRY(launch_cull(src, n, az, (int)g->z_begin, (int)g->z_end, prm->slab_halo, c->cull_win.p,
-                            c->cull_cnt.p, dst, nullptr, s));
+                            c->cull_cnt.p, c->cull_mask.p, dst, nullptr, s));
         // the kept particles' bounding box (with the slab's query planes) from the count on the device,
         // read back with the count: one host synchronisation for the cull and the cell grid
         PTV_TRY(c->bbox_part.ensure(6 * 1024));

@@ -331,7 +331,7 @@ __global__ __launch_bounds__(256) void k_place(const uint32_t *__restrict__ inv,
 // keep the particles with z in [min(az[z0..z1)) - halo, max(az[z0..z1)) + halo], in their
 // original relative order (order-preserving compaction: per-block counts, scan, write)
 // ---------------------------------------------------------------------------
-constexpr int kCullItems = 16;
+constexpr int kCullItems = 4;  // particles per thread (16 measured 87 us for the write pass at 5M, latency-bound)
 constexpr int kCullTile = 256 * kCullItems;  // particles per block
 
 // win[0..3] = (zlo, zhi, slab z min, slab z max)
@@ -377,22 +377,25 @@ __device__ __forceinline__ bool cull_keep(const double *__restrict__ x, const do
     return v > hi ? v <= m.top[c] : v >= m.bot[c];  // NaN coordinates: never kept
 }
 
+// pass 1: the keep test of every particle, one ballot mask per (block item, wave) and the block's count
 __global__ __launch_bounds__(256) void k_cull_count(const double *__restrict__ x, const double *__restrict__ y,
                                                     const double *__restrict__ z, int64_t n,
                                                     const double *__restrict__ win, CullMap m,
-                                                    uint32_t *__restrict__ bcount) {
+                                                    uint32_t *__restrict__ bcount,
+                                                    unsigned long long *__restrict__ masks) {
     const double lo = win[0], hi = win[1];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int64_t base = (int64_t)blockIdx.x * kCullTile + threadIdx.x;
     uint32_t c = 0;
 #pragma unroll
     for (int j = 0; j < kCullItems; ++j) {
         const int64_t i = base + (int64_t)j * 256;
-        if (i < n) c += cull_keep(x, y, z, i, lo, hi, m) ? 1u : 0u;
+        const unsigned long long bm = __builtin_amdgcn_ballot_w64(i < n && cull_keep(x, y, z, i, lo, hi, m));
+        if (lane == 0) masks[((size_t)blockIdx.x * kCullItems + j) * 4 + wid] = bm;
+        c += (uint32_t)__builtin_popcountll(bm);
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
     __shared__ uint32_t ws[4];
-    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+    if (lane == 0) ws[wid] = c;
     __syncthreads();
     if (threadIdx.x == 0) bcount[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
 }
@@ -402,56 +405,55 @@ struct Cols6 {
     double *dst[6];
 };
 
-// item (j, thread) of a block is particle base + j*256 + thread: j-major, thread-minor is
-// index order, so the ranks below preserve it
-__global__ __launch_bounds__(256) void k_cull_write(Cols6 c, int64_t n, const double *__restrict__ win, CullMap m,
+// pass 2 (after the scan of the counts): the kept particles' six columns from pass 1's masks.
+// Item (j, thread) of a block is particle base + j*256 + thread: j-major, thread-minor is index
+// order, so the ranks below preserve it
+__global__ __launch_bounds__(256) void k_cull_write(Cols6 c, int64_t n, const unsigned long long *__restrict__ masks,
                                                     const uint32_t *__restrict__ boff) {
-    const double lo = win[0], hi = win[1];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    __shared__ uint32_t wcnt[kCullItems][4];
     const int64_t base = (int64_t)blockIdx.x * kCullTile + threadIdx.x;
-    bool keep[kCullItems];
-#pragma unroll
-    for (int j = 0; j < kCullItems; ++j) {
-        const int64_t i = base + (int64_t)j * 256;
-        keep[j] = false;
-        if (i < n) keep[j] = cull_keep(c.src[0], c.src[1], c.src[2], i, lo, hi, m);
-        const unsigned long long m = __builtin_amdgcn_ballot_w64(keep[j]);
-        if (lane == 0) wcnt[j][wid] = (uint32_t)__builtin_popcountll(m);
-    }
-    __syncthreads();
+    const unsigned long long *bm = masks + (size_t)blockIdx.x * kCullItems * 4;
     uint32_t off = boff[blockIdx.x];
 #pragma unroll
     for (int j = 0; j < kCullItems; ++j) {
-        const unsigned long long m = __builtin_amdgcn_ballot_w64(keep[j]);
+        const unsigned long long w0 = bm[j * 4], w1 = bm[j * 4 + 1], w2 = bm[j * 4 + 2], w3 = bm[j * 4 + 3];
+        const unsigned long long m = wid == 0 ? w0 : (wid == 1 ? w1 : (wid == 2 ? w2 : w3));
         uint32_t pre = off;
-        for (int w = 0; w < wid; ++w) pre += wcnt[j][w];
-        if (keep[j]) {
+        if (wid > 0) pre += (uint32_t)__builtin_popcountll(w0);
+        if (wid > 1) pre += (uint32_t)__builtin_popcountll(w1);
+        if (wid > 2) pre += (uint32_t)__builtin_popcountll(w2);
+        if ((m >> lane) & 1ull) {
             const uint32_t r = pre + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
             const int64_t i = base + (int64_t)j * 256;
 #pragma unroll
             for (int a = 0; a < 6; ++a) c.dst[a][r] = c.src[a][i];
         }
-        off += wcnt[j][0] + wcnt[j][1] + wcnt[j][2] + wcnt[j][3];
+        off += (uint32_t)(__builtin_popcountll(w0) + __builtin_popcountll(w1) + __builtin_popcountll(w2) +
+                          __builtin_popcountll(w3));
     }
+    (void)n;
 }
 
 size_t cull_blocks(int64_t n) { return (size_t)((n + kCullTile - 1) / kCullTile); }
 
+size_t cull_mask_words(int64_t n) { return cull_blocks(n) * kCullItems * 4; }
+
 int launch_cull(const double *const src[6], int64_t n, const double *az, int z0, int z1, double halo, double *win,
-                uint32_t *bcount, double *const dst[6], uint32_t *h_total, hipStream_t s, const CullMap *map) {
+                uint32_t *bcount, unsigned long long *masks, double *const dst[6], uint32_t *h_total, hipStream_t s,
+                const CullMap *map) {
     const int nb = (int)cull_blocks(n);
     const CullMap m = map != nullptr ? *map : CullMap{};
     hipLaunchKernelGGL(k_slab_window, dim3(1), dim3(256), 0, s, az, z0, z1, map != nullptr ? 0.0 : halo, win);
     hipLaunchKernelGGL(k_cull_count, dim3(nb), dim3(256), 0, s, src[0], src[1], src[2], n, (const double *)win, m,
-                       bcount);
+                       bcount, masks);
     hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(1024), 0, s, bcount, nb);  // total -> bcount[nb]
     Cols6 c;
     for (int a = 0; a < 6; ++a) {
         c.src[a] = src[a];
         c.dst[a] = dst[a];
     }
-    hipLaunchKernelGGL(k_cull_write, dim3(nb), dim3(256), 0, s, c, n, (const double *)win, m, (const uint32_t *)bcount);
+    hipLaunchKernelGGL(k_cull_write, dim3(nb), dim3(256), 0, s, c, n, (const unsigned long long *)masks,
+                       (const uint32_t *)bcount);
     PTV_HIP(hipGetLastError());
     if (h_total != nullptr) PTV_HIP(hipMemcpyAsync(h_total, bcount + nb, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     return PTV_OK;
@@ -583,6 +585,25 @@ __global__ __launch_bounds__(256) void k_cull_map_final(const unsigned long long
     }
     if (utop != nullptr && __builtin_amdgcn_ballot_w64(short_) != 0 && (threadIdx.x & 63) == 0)
         atomicMax(fail, (unsigned long long)__double_as_longlong(INFINITY));
+}
+
+// the cull proof of a call with the cached map: the map is monotone in the lattice bounds, so
+// every bound of this call within `factor` of the bound the map was built from proves it (the
+// lattice points are the same: the cache key holds the grid and the slab).  *fail as launch_cull_need.
+__global__ __launch_bounds__(256) void k_bounds_within(const double *__restrict__ dk, const double *__restrict__ ref,
+                                                       long long n, double factor, unsigned long long *__restrict__ fail) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    const bool bad = i < n && !(dk[i] <= ref[i] * factor);
+    if (__builtin_amdgcn_ballot_w64(bad) != 0 && (threadIdx.x & 63) == 0)
+        atomicMax(fail, (unsigned long long)__double_as_longlong(INFINITY));
+}
+
+int launch_bounds_within(const double *dk, const double *ref, long long n, double factor, unsigned long long *fail,
+                         hipStream_t s) {
+    PTV_HIP(hipMemsetAsync(fail, 0, sizeof(unsigned long long), s));
+    hipLaunchKernelGGL(k_bounds_within, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, dk, ref, n, factor, fail);
+    PTV_HIP(hipGetLastError());
+    return PTV_OK;
 }
 
 int launch_cull_need(const double *lax, const double *lay, const double *laz, const int n[3], const double *dk,

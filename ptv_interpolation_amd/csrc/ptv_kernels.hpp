@@ -34,9 +34,10 @@ struct CullMap {
     int mx = 0, my = 0;
     double x0 = 0.0, y0 = 0.0, cw = 1.0, ch = 1.0, icw = 1.0, ich = 1.0;
 };
-// map != NULL: the per-column map replaces the scalar halo
+// map != NULL: the per-column map replaces the scalar halo; masks: cull_mask_words(n) scratch words
+size_t cull_mask_words(int64_t n);
 int launch_cull(const double *const src[6], int64_t n, const double *az, int z0, int z1, double halo, double *win,
-                uint32_t *bcount, double *const dst[6], uint32_t *h_total, hipStream_t s,
+                uint32_t *bcount, unsigned long long *masks, double *const dst[6], uint32_t *h_total, hipStream_t s,
                 const CullMap *map = nullptr);
 // the map a slab needs, from its finest lattice (axes lax / lay / laz, n[3] points, k-th distance
 // bounds dk over the particles binned): top / bot per cell of m's geometry; cols: 7 (n0-1)(n1-1)
@@ -44,6 +45,9 @@ int launch_cull(const double *const src[6], int64_t n, const double *az, int z0,
 // With `used` (the map the binned particles were culled with) *fail is set to 0 when the need fits
 // inside it everywhere (the cull is proven exact), else to +inf's bits (the slab_halo gate's
 // convention).
+// *fail = 0 when dk[i] <= ref[i] * factor for every i < n, else +inf's bits (the cached cull map's proof)
+int launch_bounds_within(const double *dk, const double *ref, long long n, double factor, unsigned long long *fail,
+                         hipStream_t s);
 int launch_cull_need(const double *lax, const double *lay, const double *laz, const int n[3], const double *dk,
                      double mg, double slack, const CullMap &m, double *top, double *bot, double *cols,
                      unsigned long long *keys, const CullMap *used, unsigned long long *fail, hipStream_t s);

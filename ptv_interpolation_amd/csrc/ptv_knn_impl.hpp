@@ -2372,6 +2372,7 @@ __global__ __launch_bounds__(256) void k_kdist_merge(KnnKernelArgs a, const doub
 #pragma unroll
     for (int j = 0; j < (KEYS ? 1 : KMAX); ++j) bp[j] = -1;
     const uint32_t *in = a.split_out + (size_t)t * a.split * KMAX * 64 + lane;
+#pragma unroll 2
     for (int p = 0; p < a.split; ++p) {
 #pragma unroll
         for (int j = 0; j < KMAX; ++j) {

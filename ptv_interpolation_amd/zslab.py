@@ -134,3 +134,46 @@ def gather_field(slab, dist=None, counts=None):
         full[off:off + c] = padded[r * pmax:r * pmax + c]
         off += c
     return full
+
+
+def balanced_bounds(bounds, times, min_planes: int = 12):
+    """Re-cut a z-slab partition so that every rank gets the same share of the measured cost.
+
+    ``bounds``: the current N + 1 plane boundaries (0 = b0 < b1 < ... < bN = nz); ``times``: each
+    rank's measured step time on its slab.  The cost is modelled as uniform within each current
+    slab (time / planes), the cumulative cost is cut at k / N of the total, and every slab keeps at
+    least ``min_planes`` planes (the slab lattice needs >= 9; fewer would lose the cull proof).
+    Repeated after each re-measure, the cut converges on slabs of varying cost density (the sphere
+    pack's void planes cost more per plane than its packed ones)."""
+    bounds = [int(b) for b in bounds]
+    n = len(bounds) - 1
+    nz = bounds[-1]
+    if n <= 1 or len(times) != n:
+        return bounds
+    min_planes = max(1, min(int(min_planes), nz // n))
+    dens = []
+    for r in range(n):
+        w = bounds[r + 1] - bounds[r]
+        dens.append(max(float(times[r]), 0.0) / w if w > 0 else 0.0)
+    cum = [0.0]
+    for r in range(n):
+        cum.append(cum[-1] + dens[r] * (bounds[r + 1] - bounds[r]))
+    total = cum[-1]
+    if not (total > 0.0):
+        return bounds
+
+    def plane_at(c):  # the (fractional) plane where the cumulative cost reaches c
+        for r in range(n):
+            if c <= cum[r + 1] or r == n - 1:
+                d = dens[r]
+                return bounds[r] + ((c - cum[r]) / d if d > 0 else 0.0)
+        return float(nz)
+
+    new = [0]
+    for r in range(1, n):
+        z = int(round(plane_at(total * r / n)))
+        z = max(z, new[-1] + min_planes)
+        z = min(z, nz - (n - r) * min_planes)
+        new.append(z)
+    new.append(nz)
+    return new

@@ -44,6 +44,12 @@ def test_gpus_flag_spawns_ranks(n, grid):
     assert edges[0] == 0 and edges[-1] == grid and all(a < b for a, b in zip(edges, edges[1:]))
     assert max(b - a for a, b in line["partition"]) - min(b - a for a, b in line["partition"]) <= 1
     assert line["particles_agree"] and line["field_reassembled"]
+    # the warmup re-cut: every rank derives the same boundaries from the all-gathered step times,
+    # and they even out the (synthetic) cost
+    bal = line["balanced"]
+    assert bal["ranks_agree"] and bal["bounds"][0] == 0 and bal["bounds"][-1] == grid
+    assert all(a < b for a, b in zip(bal["bounds"], bal["bounds"][1:]))
+    assert bal["cost_spread"][-1] <= bal["cost_spread"][0]
 
 
 def test_world_size_mismatch_fails_loudly():
@@ -78,3 +84,22 @@ def test_share_and_world_checks():
     # the default headline is strong scaling of the ONE named grid; weak stacking is opt-in
     assert bench.CONFIGS["headline"]["scaling"] == "strong"
     assert bench.CONFIGS["headline_weak"]["scaling"] == "weak"
+
+
+def test_balanced_bounds_evens_out_the_cost():
+    """zslab.balanced_bounds: a cut of the measured cost at k/N of the total, at least min_planes per
+    slab, boundaries strictly increasing and covering the grid."""
+    from ptv_interpolation_amd import zslab
+
+    nz, n = 512, 8
+    dens = [1.0 + (1.5 if 128 <= z < 200 or 320 <= z < 384 else 0.0) for z in range(nz)]
+    b = [nz * r // n for r in range(n + 1)]
+    spreads = []
+    for _ in range(3):
+        t = [sum(dens[b[r]:b[r + 1]]) for r in range(n)]
+        spreads.append(max(t) / min(t))
+        b = zslab.balanced_bounds(b, t)
+        assert b[0] == 0 and b[-1] == nz and all(y - x >= 12 for x, y in zip(b, b[1:]))
+    t = [sum(dens[b[r]:b[r + 1]]) for r in range(n)]
+    assert max(t) / min(t) < 1.1 < spreads[0]
+    assert zslab.balanced_bounds([0, 10, 20], [1.0]) == [0, 10, 20]  # mismatched input: unchanged
