@@ -86,6 +86,7 @@ struct ptv_ctx {
     DevBuf<uint32_t> slots;                                      // local RBF: chunk k-NN slots
     DevBuf<int> rbf_pw, rbf_status;                              // monomial exponents, singular count
     DevBuf<uint32_t> rbf_nslist;                                 // local RBF: voxels k_rbf_ns hands over
+    DevBuf<int> rbf_cflag;                                       // local RBF: per chunk flagged / overflow
     DevBuf<double> smooth;                                       // per-particle smoothing (host calls)
     DevBuf<uint8_t> fld[4];                                      // divergence host calls: U, V, W, out
     DevBuf<double> mask_axes;                                    // sample_mask: raw axes (ascending)
@@ -239,6 +240,7 @@ int ptv_free(ptv_ctx *c) {
     c->rbf_pw.release();
     c->rbf_status.release();
     c->rbf_nslist.release();
+    c->rbf_cflag.release();
     c->lin_simp.release();
     c->lin_nbr.release();
     c->lin_v2s.release();
@@ -1091,16 +1093,24 @@ int run_rbf(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_rbf
     ra.smoothing = prm->smoothing;
     ra.flags = prm->flags;
     int st_out[6] = {0, 0, 0, 0, 0, 0};
-    bool ns_overflow = false;  // pass 0's null-space list overflowed: pass 1 pivots every voxel
+    // per chunk: the voxels k_rbf_ns flagged (status[3] of its launch) and whether they overflowed
+    // the list (status[4]), copied on the device after each chunk
+    PTV_TRY(c->rbf_cflag.ensure(2 * (size_t)nchunks));
+    std::vector<int> cflag(2 * (size_t)nchunks, 0);
+    std::vector<char> rerun((size_t)nchunks, 1);
+    int64_t pivoted = 0;
     for (int pass = 0; pass < 2; ++pass) {
-    // pass 1 (rare): k_rbf_spd16 met a pivot its reciprocal does not serve, or k_rbf_ns flagged more
-    // voxels in a chunk than its list holds; redo every chunk with the LDS-broadcast SPD kernel (same
-    // arithmetic plus the IEEE division for such pivots) and without the null-space kernel
+    // pass 1 (rare): k_rbf_spd16 met a pivot its reciprocal does not serve (every chunk again with the
+    // LDS-broadcast SPD kernel: the same arithmetic plus the IEEE division for such pivots), or
+    // k_rbf_ns flagged more voxels in a chunk than its list holds (that chunk again, pivoting)
     ra.spd_lds = pass;
     ra.ns_list = pass == 0 ? c->rbf_nslist.p : nullptr;
     ra.ns_cap = kRbfNsCap;
-    PTV_HIP(hipMemcpyAsync(c->rbf_status.p, st_init, sizeof(st_init), hipMemcpyHostToDevice, s));
+    // (a full SPD rerun starts its counts afresh; an overflow rerun adds to pass 0's)
+    if (pass == 0 || st_out[2] != 0)
+        PTV_HIP(hipMemcpyAsync(c->rbf_status.p, st_init, sizeof(st_init), hipMemcpyHostToDevice, s));
     for (int ch = 0; ch < nchunks; ++ch) {
+        if (!rerun[ch]) continue;
         const int za = (int)(z0 + (int64_t)ch * cp), zb = (int)std::min<int64_t>(z1, za + cp);
         KnnLaunch cl = kl;
         cl.z0 = za;
@@ -1115,18 +1125,34 @@ int run_rbf(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_rbf
         ra.z1 = zb;
         PTV_TRY(launch_rbf(ra, b, c->slots.p, ax, ay, az, qx, qy, qz, smooth, c->rbf_pw.p, mask, U, V, W,
                            c->rbf_status.p, s));
+        if (pass == 0) {
+            PTV_HIP(hipMemcpyAsync(c->rbf_cflag.p + 2 * ch, c->rbf_status.p + 3, 2 * sizeof(int),
+                                   hipMemcpyDeviceToDevice, s));
+            PTV_HIP(hipMemsetAsync(c->rbf_status.p + 4, 0, sizeof(int), s));
+        }
         PTV_HIP(hipEventRecord(c->rbf_ev[3 * ch + 2], s));
     }
     PTV_HIP(hipMemcpyAsync(st_out, c->rbf_status.p, sizeof(st_out), hipMemcpyDeviceToHost, s));
+    if (pass == 0)
+        PTV_HIP(hipMemcpyAsync(cflag.data(), c->rbf_cflag.p, cflag.size() * sizeof(int), hipMemcpyDeviceToHost, s));
     PTV_HIP(hipStreamSynchronize(s));
-    if (st_out[2] == 0 && st_out[4] == 0) break;
-    ns_overflow = st_out[4] != 0;
+    if (pass == 1) break;
+    bool again = false;
+    for (int ch = 0; ch < nchunks; ++ch) {
+        const int za = (int)(z0 + (int64_t)ch * cp), zb = (int)std::min<int64_t>(z1, za + cp);
+        const bool over = cflag[2 * ch + 1] != 0;
+        // voxels the pivoting kernel solved: the flagged ones, or every voxel of an overflowed chunk
+        pivoted += over ? (int64_t)(zb - za) * plane : cflag[2 * ch];
+        rerun[ch] = (st_out[2] != 0 || over) ? 1 : 0;
+        again = again || rerun[ch];
+    }
+    if (st_out[2] != 0) pivoted = 0;  // the SPD rerun: no null-space kernel ran
+    if (!again) break;
     }
     c->rbf_chunks = nchunks;
     *n_singular = st_out[0];
     c->last.n_singular = st_out[0];
-    // voxels solved by the pivoting kernel after k_rbf_ns flagged them (every voxel of a rerun pass)
-    c->last.n_rbf_pivoted = ns_overflow ? (z1 - z0) * plane : st_out[5];
+    c->last.n_rbf_pivoted = pivoted;
     if (st_out[0] > 0) {
         set_error("Singular matrix. (" + std::to_string(st_out[0]) + " voxel system(s), first at linear voxel " +
                   std::to_string(st_out[1]) + ")");

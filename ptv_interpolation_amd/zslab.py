@@ -3,14 +3,19 @@ BASELINE north_star; replaces the reference's process fan-out, interpolator.py:1
 
 One process per GPU.  Rank r of P computes planes ``slab_bounds(nz, P)[r]`` of the grid.
 Every rank holds the whole particle set in HBM (replicated once with an RCCL all-gather or
-broadcast, outside the timed step) and the library bins only the particles within
-``slab_halo`` of its slab (``ptv_knn_params.slab_halo``: on-device compaction, then a proof
-from the coarse-lattice k-th distance bounds that no culled particle can be among any slab
-voxel's k nearest).  When the proof fails the call returns ``PTV_E_INEXACT`` with the halo it
-would have needed; ``interp_slab`` retries with that halo (a superset of the particles can only
-lower the bound, so one retry suffices) and, as a last resort, bins everything.  No collective
-touches the interpolation itself; an all-gather reassembles the full field only when a caller
-wants it on every device (``gather_field``).
+broadcast, outside the timed step) and the library bins only the particles that can reach
+its slab.  Default (bench.py, the drop-in launcher): the per-column cull map of
+``PTV_FLAG_SLAB_CULL_AUTO``, which the library derives from the slab's own lattice bounds, caches
+per context and proves exact on the device before every main launch.  The scalar
+``ptv_knn_params.slab_halo`` path remains: on-device compaction to the particles within the halo
+of the slab's z extent, then a proof from the coarse-lattice k-th distance bounds that no culled
+particle can be among any slab voxel's k nearest; when it fails the call returns
+``PTV_E_INEXACT`` with the halo it would have needed, and ``interp_slab`` retries with at least
+1.25x the refused halo (the requirement is computed on a different particle set and lattice each
+time, so it can grow over two or three retries) and, as a last resort, bins everything.  No
+collective touches the interpolation itself; an all-gather reassembles the full field only when a
+caller wants it on every device (``gather_field``).  ``balanced_bounds`` re-cuts the slabs from
+measured step times (bench.py's warmup).
 
 The functions take torch tensors / a ``torch.distributed`` module, so the same partition code
 runs over RCCL on the GPUs (bench.py) and over gloo on the CPU (tests/test_distributed.py,

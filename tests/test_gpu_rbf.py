@@ -404,6 +404,34 @@ def test_nullspace_list_overflow_reruns_with_pivoting(ctx):
         assert normwise(a, b) <= TOL
 
 
+def test_nullspace_overflow_reruns_only_its_chunk(ctx):
+    """Two z-chunks (chunk_planes=20 over 40 planes): extreme smoothing on the particles below
+    z = 18 makes the first chunk flag more voxels than the 16384-entry list holds, so that chunk
+    alone is re-solved by the pivoting kernel; the second keeps the null-space solve.  The stats
+    count every voxel of the rerun chunk plus the second chunk's flagged ones, and the result
+    matches the oracle."""
+    from oracle import cpu_ref
+
+    rng = np.random.default_rng(72)
+    P = rng.uniform(-0.5, 32.5, (40000, 3))
+    P[:, 2] = rng.uniform(-0.5, 40.5, 40000)
+    Q = rng.standard_normal((40000, 3))
+    sm = np.where(P[:, 2] < 18.0, 2e307, 0.0)
+    ax, az = np.arange(32, dtype=np.float64), np.arange(40, dtype=np.float64)
+    U, V, W = ctx.interp_rbf(P, Q, axes=(ax, ax, az), k=20, smoothing=sm, chunk_planes=20)
+    npiv = ctx.stats["n_rbf_pivoted"]
+    print("voxels solved by the pivoting kernel:", npiv)
+    assert 20 * 32 * 32 <= npiv < 40 * 32 * 32
+    rng2 = np.random.default_rng(3)
+    sel = rng2.integers(0, 40 * 32 * 32, 2000)
+    iz, iy, ix = np.unravel_index(sel, (40, 32, 32))
+    q = np.stack([ax[ix], ax[iy], az[iz]], -1)
+    ref = cpu_ref.rbf_local_points(P, Q, q, 20, smoothing=sm)
+    for c, a in enumerate((U, V, W)):
+        assert np.isfinite(a).all()
+        assert normwise(a.ravel()[sel], ref[:, c]) <= TOL
+
+
 @pytest.mark.parametrize("shape", [(1, 1, 1), (1, 1, 3), (2, 3, 5), (1, 7, 1)])
 @pytest.mark.parametrize("kernel,k,eps,degree", [
     ("thin_plate_spline", 20, None, None),  # k_rbf_ns<20, 4>
