@@ -405,18 +405,20 @@ def test_nullspace_list_overflow_reruns_with_pivoting(ctx):
 
 
 def test_nullspace_overflow_reruns_only_its_chunk(ctx):
-    """Two z-chunks (chunk_planes=20 over 40 planes): extreme smoothing on the particles below
-    z = 18 makes the first chunk flag more voxels than the 16384-entry list holds, so that chunk
+    """Two z-chunks (chunk_planes=20 over 40 planes): smoothing above the null-space kernel's 2^26
+    limit on the particles below z = 18 makes the first chunk flag more voxels than the 16384-entry
+    list holds, so that chunk
     alone is re-solved by the pivoting kernel; the second keeps the null-space solve.  The stats
-    count every voxel of the rerun chunk plus the second chunk's flagged ones, and the result
-    matches the oracle."""
+    count every voxel of the rerun chunk plus the second chunk's flagged ones.  The mixed smoothing
+    (1e8 next to 0) leaves the systems ill-conditioned, so the bar is the C3 one: gpu-vs-exact within
+    max(1e-10, lapack-vs-exact) per component (extended-precision truth of the same systems)."""
     from oracle import cpu_ref
 
     rng = np.random.default_rng(72)
     P = rng.uniform(-0.5, 32.5, (40000, 3))
     P[:, 2] = rng.uniform(-0.5, 40.5, 40000)
     Q = rng.standard_normal((40000, 3))
-    sm = np.where(P[:, 2] < 18.0, 2e307, 0.0)
+    sm = np.where(P[:, 2] < 18.0, 1e8, 0.0)
     ax, az = np.arange(32, dtype=np.float64), np.arange(40, dtype=np.float64)
     U, V, W = ctx.interp_rbf(P, Q, axes=(ax, ax, az), k=20, smoothing=sm, chunk_planes=20)
     npiv = ctx.stats["n_rbf_pivoted"]
@@ -426,10 +428,14 @@ def test_nullspace_overflow_reruns_only_its_chunk(ctx):
     sel = rng2.integers(0, 40 * 32 * 32, 2000)
     iz, iy, ix = np.unravel_index(sel, (40, 32, 32))
     q = np.stack([ax[ix], ax[iy], az[iz]], -1)
-    ref = cpu_ref.rbf_local_points(P, Q, q, 20, smoothing=sm)
+    lap = cpu_ref.rbf_local_points(P, Q, q, 20, smoothing=sm)
+    ext = cpu_ref.rbf_local_points(P, Q, q, 20, smoothing=sm, solver="extended")
     for c, a in enumerate((U, V, W)):
         assert np.isfinite(a).all()
-        assert normwise(a.ravel()[sel], ref[:, c]) <= TOL
+        got = a.ravel()[sel]
+        e_exact, gap = normwise(got, ext[:, c]), normwise(lap[:, c], ext[:, c])
+        print(f"{'UVW'[c]}: gpu-vs-exact {e_exact:.3e}  lapack-vs-exact {gap:.3e}")
+        assert e_exact <= max(TOL, gap)
 
 
 @pytest.mark.parametrize("shape", [(1, 1, 1), (1, 1, 3), (2, 3, 5), (1, 7, 1)])
