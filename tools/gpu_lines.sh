@@ -13,6 +13,14 @@ run() {  # name, time limit, bench args...  (LINES="a b c" runs only those)
   echo "== $name: bench.py $*"
   timeout -k 10 "$lim" python -u bench.py "$@" > "$out/$name.json" 2> "$out/$name.err" || { echo "FAILED $name"; tail -5 "$out/$name.err"; exit 1; }
   tail -c 400 "$out/$name.json"; echo
+  if [ -n "$KT" ]; then  # the same line again under rocprofv3 kernel-trace: its kernels' durations
+    export TMPDIR=/tmp
+    rm -rf "$out/kt_$name"
+    timeout -k 10 "$lim" rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kt_$name" -- python3 bench.py "$@" \
+      --no-cpu-baseline --no-e2e > "$out/kt_$name.log" 2>&1 || { echo "FAILED kt $name"; tail -5 "$out/kt_$name.log"; exit 1; }
+    python3 tools/kt_summary.py "$out/kt_$name" 12 > "$out/$name.kt.txt" && head -4 "$out/$name.kt.txt"
+    find "$out/kt_$name" -name "*kernel_trace.csv" -delete
+  fi
 }
 run headline 300
 run nearest 300 --method nearest --no-e2e
