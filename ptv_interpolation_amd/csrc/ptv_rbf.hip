@@ -116,6 +116,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M <= 32 ? 3
     if (a.vlist != nullptr) {  // list mode: the voxels k_rbf_ns handed over (count on the device)
         const long long n = min((long long)*a.vcount, (long long)a.ns_cap);
         valid = v < n;
+        // the grid is sized for the whole list: waves past the count leave at once (the solve below
+        // is branch-free, and 16384 voxels of it cost ~0.1 ms per chunk when the list is empty)
+        if (__builtin_amdgcn_ballot_w64(valid) == 0) return;
         v = valid ? (long long)a.vlist[v] : 0;
     }
     const long long vc = valid ? v : nvox - 1;
