@@ -82,7 +82,8 @@ METRIC_MASK = ("Mvoxels/s + achieved HBM GB/s, pore-mask path (sample_mask_on_gr
                "interpolator.py:205-284), 512³ mask")
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec (AMD); not listed in the guide
-KMAX_LIST = (4, 8, 12, 16, 24, 32, 40, 48, 56, 64)  # k_knn_interp instantiations (ptv_knn.hip)
+KMAX_EXACT = (1, 4, 8, 12)  # k_knn_interp list lengths (ptv_knn.hip kmax_for): pair lists serve k <= length,
+KMAX_KEYS = (16, 24, 32, 40, 48, 56, 64, 96, 128)  # packed-key lists k + 1 <= length
 
 # BASELINE.json configs; C1 (64^3 / 10k, CPU plumbing) is a parity test case
 CONFIGS = {
@@ -101,7 +102,7 @@ CONFIGS = {
 
 
 def kmax_for(k):
-    return next((m for m in KMAX_LIST if k <= m), 0)
+    return next((m for m in KMAX_EXACT if k <= m), 0) or next((m for m in KMAX_KEYS if k + 1 <= m), 0)
 
 
 def rbf_resolved(args):

@@ -214,7 +214,7 @@ int launch_block_order(const double *dk_coarse, const int nc[3], int nx, int ny,
 
 // list lengths: exact (d2, slot) pair lists serve k <= 12 (length >= k); packed-key lists
 // serve 13 <= k <= 127 (length >= k + 1: the near-tie slot)
-static const int kKmaxExact[] = {4, 8, 12};
+static const int kKmaxExact[] = {1, 4, 8, 12};
 static const int kKmaxKeys[] = {16, 24, 32, 40, 48, 56, 64, 96, 128};
 
 int kmax_for(int k) {
@@ -231,6 +231,7 @@ int kmax_for(int k) {
     extern template void launch_t<K, E>(dim3, hipStream_t, const KnnKernelArgs &, const Binned &, const double *, \
                                         const double *, const double *, const double *, const double *,        \
                                         const double *, const uint8_t *, double *, double *, double *);
+PTV_KNN_EXTERN(1, false)
 PTV_KNN_EXTERN(4, false)
 PTV_KNN_EXTERN(8, false)
 PTV_KNN_EXTERN(12, false)
@@ -268,6 +269,7 @@ static int launch_kmax(int km, bool exact, dim3 grid, hipStream_t s, const KnnKe
         }                                                                                    \
         launch_t<K, false>(grid, s, ka, b, ax, ay, az, qx, qy, qz, mask, U, V, W);           \
         break;
+        PTV_CASE(1)
         PTV_CASE(4)
         PTV_CASE(8)
         PTV_CASE(12)
