@@ -91,6 +91,16 @@ constexpr int kStampFields = 8;
 // lattice levels: insertions per group that pay for the fp32 k-th network (same-box A/B, 512^3 / 5M:
 // lattice 1.86 ms without it, 1.80 at 16, 1.72 at 32; C2 and the 2/8 share unchanged)
 constexpr int kTightenMin = PTV_TIGHTEN_MIN;
+#ifndef PTV_TIGHTEN_KEYS
+// dev builds: key-list modes that tighten a group's threshold first (1 = filter, 2 = interp).  Off:
+// same-box A/B at 512^3 / 5M, filter k = 25 19.80 -> 20.52 ms, Sibson k = 30 55.2 -> 60.3, IDW k = 50
+// 104.0 -> 121.8 (the key lists' thresholds are already tight after the first group)
+#define PTV_TIGHTEN_KEYS 0
+#endif
+template <int MODE>
+constexpr bool tighten_keys() {
+    return (MODE == kModeFilter && (PTV_TIGHTEN_KEYS & 1)) || (MODE == kModeInterp && (PTV_TIGHTEN_KEYS & 2));
+}
 constexpr int kCap = 128;        // LDS candidate slots per wave (16 B fp32 + 32 B fp64 each)
 constexpr int kRowsPerLane = 1;  // cell rows examined per lane per gather round
 constexpr int kRunEntries = 64 * 2 * kRowsPerLane;  // x-runs per gather round (power of two)
@@ -196,8 +206,8 @@ __device__ __forceinline__ void insert_key(double (&bd)[KMAX], double key) {
 // Keys are distinct (the slot is part of the key), so the list equals the sequential one.
 struct KeyNet {
     int n;
-    short a[1024], b[1024];
-    unsigned char kind[1024];  // 1: a = min only, 2: b = max only, 3: both
+    short a[1536], b[1536];    // up to the 1471 comparators of a full 128-entry sort (SortNetOf)
+    unsigned char kind[1536];  // 1: a = min only, 2: b = max only, 3: both
 };
 struct RegList {
     int n;
@@ -276,7 +286,7 @@ constexpr KeyNet make_key_net() {
     }
     if (net.n < 0) return net;
     KeyNet res{};
-    int keep[1024] = {};
+    int keep[1536] = {};
     for (int c = net.n - 1; c >= 0; --c) {
         const bool la = live[net.a[c]], lb = live[net.b[c]];
         keep[c] = c < nsort ? 3 : (la ? 1 : 0) | (lb ? 2 : 0);
@@ -330,6 +340,76 @@ __device__ __forceinline__ void insert_keys(double (&bd)[KMAX], const double (&n
     key_net_run<KMAX, NB>(v, std::make_integer_sequence<int, KeyNetOf<KMAX, NB>::net.n>{});
 #pragma unroll
     for (int j = 0; j < KMAX; ++j) bd[j] = v[j];
+}
+
+// Full sort of KMAX registers (net_sort: Batcher's odd-even merge sort, every comparator
+// ascending) and the register that holds each sorted position.
+template <int KMAX>
+struct SortNetOf {
+    static constexpr KeyNet make() {
+        KeyNet net{};
+        RegList x{}, out{};
+        for (int i = 0; i < KMAX; ++i) x.r[x.n++] = (short)i;
+        net_sort(x, net, out);
+        return net;
+    }
+    static constexpr RegList order() {
+        KeyNet net{};
+        RegList x{}, out{};
+        for (int i = 0; i < KMAX; ++i) x.r[x.n++] = (short)i;
+        net_sort(x, net, out);
+        return out;
+    }
+    static constexpr KeyNet net = make();
+    static constexpr RegList ord = order();
+};
+template <int KMAX, int C>
+__device__ __forceinline__ void sort_net_op(double (&v)[KMAX]) {
+    constexpr int a = SortNetOf<KMAX>::net.a[C], b = SortNetOf<KMAX>::net.b[C];
+    const double x = v[a], y = v[b];
+    double lo, hi;
+    asm("v_min_f64 %0, %1, %2" : "=v"(lo) : "v"(x), "v"(y));
+    asm("v_max_f64 %0, %1, %2" : "=v"(hi) : "v"(x), "v"(y));
+    v[a] = lo;
+    v[b] = hi;
+}
+template <int KMAX, int... C>
+__device__ __forceinline__ void sort_net_run(double (&v)[KMAX], std::integer_sequence<int, C...>) {
+    (sort_net_op<KMAX, C>(v), ...);
+}
+#ifndef PTV_MEDIAN_NET
+#define PTV_MEDIAN_NET 1  // dev builds: 0 = the O(KMAX^2) rank selection (ptv_median.hpp)
+#endif
+// np.median of s[0..n) for values >= +0 or NaN (the filter's speeds and absolute deviations:
+// no signed zeros, so any order of equal values gives the same bits): entries past n become
+// +inf, one sorting network, the middle one (n odd) or the mean of the two middle ones; any NaN
+// gives NaN (numpy's _median_nancheck).  191 comparators at KMAX = 32 against the rank
+// selection's 2 x 1024 compares per call.
+template <int KMAX>
+__device__ __forceinline__ double median_sorted(const double (&s)[KMAX], int n) {
+    bool nan = false;
+    double v[KMAX];
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) {
+        if (j < n) nan = nan || (s[j] != s[j]);
+        v[j] = j < n ? s[j] : INFINITY;
+    }
+    sort_net_run<KMAX>(v, std::make_integer_sequence<int, SortNetOf<KMAX>::net.n>{});
+    const int h = n >> 1;
+    double lo = 0.0, hi = 0.0;
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i) {
+        const double x = v[SortNetOf<KMAX>::ord.r[i]];
+        if (i == h - 1) lo = x;
+        if (i == h) hi = x;
+    }
+    const double m = (n & 1) ? hi : (lo + hi) / 2.0;
+    return nan ? __longlong_as_double(0x7ff8000000000000LL) : m;
+}
+template <int KMAX>
+__device__ __forceinline__ double filter_median(const double (&s)[KMAX], int n) {
+    if constexpr (PTV_MEDIAN_NET) return median_sorted<KMAX>(s, n);
+    else return median_of<KMAX>(s, n);
 }
 
 // numpy's pairwise sum (see pairwise()) fed in index order in blocks of 8 values: block m
@@ -1270,19 +1350,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                 unsigned long long m = group_mask();
                 const double4 *gbuf = buf + g0 + nb - 64;  // bit position p <-> gbuf[63 - p]
                 int nit = __builtin_amdgcn_readfirstlane(wave_max_i(__builtin_popcountll(m)));
-                if constexpr (MODE == kModeKDist && !KEYS) {
+                if constexpr ((MODE == kModeKDist && !KEYS) || (KEYS && tighten_keys<MODE>())) {
                     // lattice levels start from the coarse bound (no seeds): a lane whose list is not
                     // full yet takes every candidate under it.  When some lane would insert more than
                     // kTightenMin of this group, first each lane's k-th smallest fp32 d2 over its list
                     // and the group (fmed3 network; list entries rounded up, the group's within cpass):
                     // an upper bound on the k-th of the two, so the insertions keep to the candidates
-                    // that can stay in the list (the lists come out the same)
+                    // that can stay in the list (the lists come out the same).  Key lists (the outlier
+                    // filter, whose seeds are only its Morton blob): an entry's key times kscale bounds
+                    // its exact d2, the k-th sits at KMAX - 2, and the bound is widened by kscale so
+                    // that every candidate sharing the final k-th key's truncation still reaches the
+                    // (k+1)-th slot (the near-tie check); a candidate past it cannot be the (k+1)-th
+                    // key's near tie either.
                     if (nit > kTightenMin) {
+                        constexpr int KT = KEYS ? KMAX - 2 : KMAX - 1;  // the k-th entry
+                        const double ks = KEYS ? a.kscale : 1.0;
                         float sd[KMAX];
 #pragma unroll
                         for (int j = 0; j < KMAX; ++j)
                             sd[j] = bd[j] < 0.0 ? -1.0f
-                                                : (bd[j] < INFINITY ? (float)(bd[j] * (1.0 + 2.384185791015625e-07)) : INFINITY);
+                                                : (bd[j] < INFINITY ? (float)(bd[j] * ks * (1.0 + 2.384185791015625e-07)) : INFINITY);
                         for (int i = 0; i < ng; i += 2) {
                             const float2 X = *reinterpret_cast<const float2 *>(fbx + g0 + i);
                             const float2 Y = *reinterpret_cast<const float2 *>(fby + g0 + i);
@@ -1299,8 +1386,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                                 sd[0] = fminf(sd[0], xs[u]);
                             }
                         }
-                        if (active && sd[KMAX - 1] >= 0.0f && sd[KMAX - 1] < INFINITY) {
-                            const double t = ((double)sd[KMAX - 1] * (1.0 + 9.5367431640625e-07) + cpass) * (1.0 + 1e-12);
+                        if (active && sd[KT] >= 0.0f && sd[KT] < INFINITY) {
+                            const double t = ((double)sd[KT] * (1.0 + 9.5367431640625e-07) + cpass) * ks * (1.0 + 1e-12);
                             if (t < thr) {
                                 thr = t;
                                 thrf = f32_bound(thr, cpass);
@@ -1357,7 +1444,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                         thr = dmin(bd[KMAX - 1], ub2);
                     }
                 }
-                if constexpr (KEYS) thr = dmin(kth2(), ub2);
+                if constexpr (KEYS) thr = dmin(thr, kth2());  // thresholds only shrink (a tightened one stays)
                 thrf = f32_bound(thr, cpass);
             }
             n_surv += (uint32_t)nbuf;
@@ -1749,14 +1836,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
         double sp[KMAX];
 #pragma unroll
         for (int t = 0; t < KMAX; ++t) sp[t] = t + 1 < KMAX ? (t < drop ? v[t] : v[t + 1]) : 0.0;
-        const double med = median_of(sp, kk);
+        const double med = filter_median(sp, kk);
         double dev[KMAX];
 #pragma unroll
         for (int t = 0; t < KMAX; ++t) dev[t] = fabs(sp[t] - med);
-        const double mad = median_of(dev, kk);
+        const double mad = filter_median(dev, kk);
         const double zsc = fabs(a.fe.spd[qslot] - med) / (mad + a.fe.mad_eps);
         a.fe.keep[orig] = zsc <= a.fe.threshold ? 1 : 0;
         if (a.fe.kth != nullptr) a.fe.kth[orig] = dk1;
+        write_stamps();
         return;
     }
     if constexpr (MODE == kModeSlots) {
@@ -2393,9 +2481,10 @@ void launch_m(dim3 grid, hipStream_t s, const KnnKernelArgs &ka, const Binned &b
                      const double *ay, const double *az, const double *qx, const double *qy, const double *qz,
                      const uint8_t *mask, double *U, double *V, double *W) {
     if constexpr ((KMAX == 8 || PTV_STAMP_ALL) && MODE != kModeSlots && !EXACT) {
-        // stamps record the main launch, or the lattice-level launches under PTV_STAMP_LATTICE=1
+        // stamps record the main launch, or the lattice-level launches under PTV_STAMP_LATTICE=1,
+        // or the outlier filter's search under PTV_STAMP_LATTICE=4
         const char *sl = dev_knob("PTV_STAMP_LATTICE");
-        const int stamp_mode = (sl && sl[0] == '1') ? kModeKDist : kModeInterp;
+        const int stamp_mode = (sl && sl[0] == '1') ? kModeKDist : ((sl && sl[0] == '4') ? kModeFilter : kModeInterp);
         if (g_dbg != nullptr && MODE == stamp_mode) {
             hipLaunchKernelGGL((k_knn_interp<KMAX, true, MODE, false>), grid, dim3(256), 0, s, ka, b.prec, b.pval,
                                b.cstart, ax, ay, az, qx, qy, qz, mask, U, V, W, g_dbg, g_dbg_cap);

@@ -1,10 +1,24 @@
 #!/bin/bash
-# One GPU call: the k-NN parity tests, then a same-box A/B of a dev knob on the headline bench.
-# usage: tools/gpu_ab.sh VAR v1 v2 ...   (tests: PTV_AB_TESTS, default the parity + zslab files)
+# Same-box A/B of bench lines over dev libraries: each (library, bench args) pair run twice,
+# alternating, every run under its own time limit.  Output: gpurun_out/<tag>_ab/<lib>_<n>_<i>.json
+# usage: gpurun -- bash tools/gpu_ab.sh TAG "lib1 lib2 ..." "args1; args2; ..."   (lib "-" = shipped)
 set -o pipefail
+tag=$1; libs=$2; specs=$3
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
-mkdir -p gpurun_out
-T=${PTV_AB_TESTS:-"tests/test_gpu_parity.py tests/test_gpu_nearest_div.py tests/test_gpu_zslab.py"}
-timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread $T > gpurun_out/ab_tests.log 2>&1
-rc=$?; tail -3 gpurun_out/ab_tests.log; if [ $rc -ne 0 ]; then exit $rc; fi
-bash tools/ab_env.sh "$@"
+out=gpurun_out/${tag}_ab
+mkdir -p "$out"
+IFS=';' read -ra SP <<< "$specs"
+for i in 1 2; do
+  n=0
+  for spec in "${SP[@]}"; do
+    n=$((n + 1))
+    for lib in $libs; do
+      name=$(basename "$lib" .so)_${n}_$i
+      if [ "$lib" = "-" ]; then name=shipped_${n}_$i; unset PTV_LIB; else export PTV_LIB=$(realpath "$lib"); fi
+      timeout -k 10 300 python -u bench.py $spec --no-cpu-baseline --no-e2e > "$out/$name.json" 2> "$out/$name.err" || { echo "FAILED $name"; tail -5 "$out/$name.err"; exit 1; }
+      python3 -c "
+import json,sys; d=json.loads(open('$out/$name.json').read().strip().splitlines()[-1])
+print('$name', '$spec', d['ms_per_step'], d.get('breakdown_ms'))"
+    done
+  done
+done
