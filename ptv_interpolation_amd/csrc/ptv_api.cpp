@@ -299,7 +299,7 @@ namespace {
 constexpr double kDefaultOccupancySmallK = 16.0;  // particles per (y, z) cell column segment
 constexpr double kDefaultXRefSmallK = 12.0;       // x-refinement of the k <= 8 cells
 constexpr double kDefaultOccupancy = 1.2;          // k > 8 without lattice seeds (point lists)
-// k > 8 with union seeds (round 3, tools/gpu_knob_sweep.sh, 512^3 / 5M IDW k = 50): the seeded
+// k > 8 with union seeds (round 3, a dev-knob sweep, now tools/gpu_envab.sh, 512^3 / 5M IDW k = 50): the seeded
 // gather radius is tight, so coarser cells (fewer runs per row) win again: main launch
 // 139.7 ms at 1.2 / cubic, 137.7 at 2.5, 134.8 at 5, 133.5 at 8 with x 4x thinner, 133.4 at 16 / 12
 constexpr double kDefaultOccupancyLargeK = 8.0;
@@ -313,7 +313,7 @@ constexpr long long kLatticeStopPoints = 50000; // no coarser lattice below this
 constexpr size_t kSeedBytesMax = 40ULL << 30;    // lattice seed records per level (C5 2048^3, k = 8: 17 GB)
 // split lattice launch (k_kdist_merge): the first max(kLatticeSplitMinBlocks, blocks /
 // kLatticeSplitDiv) blocks of a lattice level's longest-first order, kLatticeSplit waves per tile.
-// Measured (512^3 / 5M sphere pack, k = 8, tools/gpu_sweep.sh): the share 2/8 lattice 1.81 ->
+// Measured (512^3 / 5M sphere pack, k = 8, a dev-knob sweep, now tools/gpu_envab.sh): the share 2/8 lattice 1.81 ->
 // 0.88 ms at 64 blocks (1.07 at 32, 2.05 at 8), C2 0.81 -> 0.69; the whole 512^3 grid's lattice
 // launch is throughput-bound (35.9k tiles of ~280k cycles each), 1.91 -> 1.86 ms
 constexpr int kLatticeSplit = 16;
