@@ -336,10 +336,16 @@ def test_nullspace_vs_pivoting_and_oracle(ctx, kernel, k, degree):
     assert ctx.stats["n_rbf_pivoted"] == 0
     piv = it.evaluate_grid(ax, ax, ax, flags=_lib.FLAG_RBF_PIVOTING)
     ref = cpu_ref.rbf_local_grid(P, Q, ax, ax, ax, k, kernel, None, degree)
+    gz, gy, gx = np.meshgrid(ax, ax, ax, indexing="ij")
+    ext = cpu_ref.rbf_local_points(P, Q, np.stack([gx.ravel(), gy.ravel(), gz.ravel()], -1), k, kernel,
+                                   degree=degree, solver="extended")
     assert any(not np.array_equal(a, b) for a, b in zip(ns, piv))
     for c, (a, b, r) in enumerate(zip(ns, piv, ref)):
         e_ns, e_piv = normwise(a, r), normwise(b, r)
-        print(f"{kernel} k={k} {'UVW'[c]}: null-space vs oracle {e_ns:.2e}, pivoting vs oracle {e_piv:.2e}")
+        x = ext[:, c]
+        t_ns, t_piv, t_lap = normwise(a.ravel(), x), normwise(b.ravel(), x), normwise(r.ravel(), x)
+        print(f"{kernel} k={k} {'UVW'[c]}: null-space vs oracle {e_ns:.2e}, pivoting vs oracle {e_piv:.2e}; "
+              f"vs exact: null-space {t_ns:.2e}, pivoting {t_piv:.2e}, lapack {t_lap:.2e}")
         assert e_ns <= TOL and e_piv <= TOL
 
 

@@ -7,7 +7,8 @@ and the extended-precision truth.
                             definite kernel with degree >= its minimum: c~2 = B^-1 (Q^T d)[r:]
                             c = Q [0; c~2],  e = R^-1 ((Q^T d)[:r] - (Q^T Phi Q)[:r, r:] c~2)
 
-Run: python tools/rbf_nullspace_proto.py
+Run: python tools/rbf_nullspace_proto.py            (fixtures + random clouds)
+     python tools/rbf_nullspace_proto.py --refine   (one step of iterative refinement)
 """
 import os
 import sys
@@ -160,6 +161,111 @@ def ns_kernel_order(lhs, rhs, k, vec):
     return out
 
 
+def ns_kernel_coeffs(lhs, rhs, k):
+    """The kernel's step order (ns_kernel_order) returning the coefficients (c, e) instead of the
+    evaluated value: c = Q [0; c~2]."""
+    C, m, _ = lhs.shape
+    r = m - k
+    A = lhs[:, :k, :k].copy()
+    P = lhs[:, :k, k:].copy()
+    d = rhs[:, :k].copy()
+    Vs, taus, betas = [], [], []
+    rows = np.arange(k)
+    for t in range(r):
+        alpha = P[:, t, t]
+        x = np.where(rows[None, :] > t, P[:, :, t], 0.0)
+        s = np.sum(x * x, axis=1)
+        b = -np.copysign(np.sqrt(alpha * alpha + s), alpha)
+        tau = np.where(s == 0.0, 0.0, (b - alpha) / b)
+        scal = np.where(s == 0.0, 0.0, 1.0 / (alpha - b))
+        v = np.where(rows[None, :] > t, P[:, :, t] * scal[:, None], np.where(rows[None, :] == t, 1.0, 0.0))
+        b = np.where(s == 0.0, alpha, b)
+        for u in range(t + 1, r):
+            w = np.sum(v * P[:, :, u], axis=1)
+            P[:, :, u] -= (tau * w)[:, None] * v
+        w = np.einsum("ci,cis->cs", v, d)
+        d -= tau[:, None, None] * v[:, :, None] * w[:, None, :]
+        Vs.append(v); taus.append(tau); betas.append(b)
+    Z = [np.einsum("cij,cj->ci", A, Vs[t]) for t in range(r)]
+    for t in range(r):
+        for s2 in range(t):
+            zv = np.sum(Z[s2] * Vs[t], axis=1)
+            vv = np.sum(Vs[s2] * Vs[t], axis=1)
+            Z[t] = Z[t] - Z[s2] * vv[:, None] - Vs[s2] * zv[:, None]
+        Z[t] = Z[t] * taus[t][:, None]
+        kk = 0.5 * taus[t] * np.sum(Vs[t] * Z[t], axis=1)
+        Z[t] = Z[t] - kk[:, None] * Vs[t]
+    for t in range(r):
+        A[:, :, r:] -= Vs[t][:, :, None] * Z[t][:, None, r:] + Z[t][:, :, None] * Vs[t][:, None, r:]
+    for c in range(r, k):
+        piv = A[:, c, c]
+        l = np.where(rows[None, :] > c, A[:, :, c] / piv[:, None], 0.0)
+        A[:, :, c + 1:] -= l[:, :, None] * A[:, c, None, c + 1:]
+        d -= l[:, :, None] * d[:, c, None, :]
+    x = np.zeros_like(d)
+    for c in range(k - 1, r - 1, -1):
+        x[:, c] = d[:, c] / A[:, c, c][:, None]
+        above = rows[None, :] < c
+        d -= np.where(above[:, :, None], A[:, :, c, None] * x[:, c, None, :], 0.0)
+    e = np.zeros((C, r, d.shape[2]))
+    rhs_e = d[:, :r].copy()
+    for t in range(r - 1, -1, -1):
+        e[:, t] = rhs_e[:, t] / betas[t][:, None]
+        rhs_e[:, :t] -= P[:, :t, t, None] * e[:, t, None, :]
+    c = apply_left(np.stack(Vs, 1), np.stack(taus, 1), x, reverse=True)
+    return np.concatenate([c, e], axis=1)
+
+
+def ns_refined(lhs, rhs, k):
+    """One step of fixed-precision iterative refinement on top of the kernel's solve: the float64
+    residual of the first k rows (the constraint rows' residual is dropped: P^T c = 0 holds to
+    rounding by construction) re-solved with the same method, the correction added."""
+    c0 = ns_kernel_coeffs(lhs, rhs, k)
+    res = rhs - np.einsum("cij,cjs->cis", lhs, c0)
+    res[:, k:] = 0.0
+    return c0 + ns_kernel_coeffs(lhs, res, k)
+
+
+def refinement_study():
+    """Null-space error against the extended-precision truth, without and with one refinement
+    step, next to LAPACK's, on uniform clouds (the kernel's voxel-centred isotropic coordinates)."""
+    from scipy.spatial import KDTree
+
+    rng = np.random.default_rng(7)
+    for kern, k in (("thin_plate_spline", 20), ("thin_plate_spline", 32), ("cubic", 14), ("linear", 30)):
+        n, G = 5000, 14
+        y = rng.uniform(-0.5, G - 0.5, (n, 3))
+        vals = rng.standard_normal((n, 3))
+        ax = np.linspace(0, G - 1, G)
+        x = grid_q(ax, ax, ax)
+        degree = max(cpu_ref.RBF_MIN_DEGREE.get(kern, -1), 0)
+        powers = cpu_ref.monomial_powers(degree)
+        phi = cpu_ref.RBF_PHI[kern]
+        m = k + powers.shape[0]
+        _, idx = KDTree(y).query(x, k)
+        idx = np.sort(idx, axis=1)
+        yn = y[idx]
+        diff = yn[:, :, None, :] - yn[:, None, :, :]
+        lhs = np.zeros((len(x), m, m))
+        lhs[:, :k, :k] = phi(np.sqrt((diff[..., 0] ** 2 + diff[..., 1] ** 2) + diff[..., 2] ** 2))
+        rel = yn - x[:, None, :]
+        P = cpu_ref._poly(rel / np.abs(rel).max(axis=(1, 2))[:, None, None], powers)
+        lhs[:, :k, k:] = P
+        lhs[:, k:, :k] = np.swapaxes(P, 1, 2)
+        rhs = np.zeros((len(x), m, 3))
+        rhs[:, :k] = vals[idx]
+        dq = x[:, None, :] - yn
+        vec = np.concatenate([phi(np.sqrt((dq[..., 0] ** 2 + dq[..., 1] ** 2) + dq[..., 2] ** 2)),
+                              cpu_ref._poly(np.zeros_like(x), powers)], axis=1)
+        ext = np.einsum("qm,qms->qs", vec.astype(np.longdouble), cpu_ref.solve_extended(lhs, rhs)).astype(float)
+        err = lambda c: max(normwise(np.einsum("qm,qms->qs", vec, c)[:, i], ext[:, i]) for i in range(3))
+        e_lap = err(np.linalg.solve(lhs, rhs))
+        e_ns = err(ns_kernel_coeffs(lhs, rhs, k))
+        e_ir = err(ns_refined(lhs, rhs, k))
+        print(f"{kern:18s} k={k:3d}: vs exact  lapack {e_lap:.2e}  null-space {e_ns:.2e} ({e_ns / e_lap:.1f}x)  "
+              f"+1 refinement step {e_ir:.2e} ({e_ir / e_lap:.1f}x)")
+
+
 def rbf_points(points, values, queries, k, kernel, epsilon=None, degree=None, smoothing=0.0, solver="ns"):
     from scipy.spatial import KDTree
 
@@ -259,4 +365,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if "--refine" in sys.argv:
+        refinement_study()
+    else:
+        main()
