@@ -138,6 +138,31 @@ __device__ __forceinline__ double phi_ns(int kern, double d2, const double2 *__r
     }
 }
 
+#ifndef PTV_NS_LDS_PAD
+#define PTV_NS_LDS_PAD 1  // dev builds: 0 = the round-4 build scratch layout (stride NC + 1, unpadded systems)
+#endif
+// LDS banks (MI355X_MICROARCH.md §LDS): ds_read_b64 serves 32 lanes (two systems) per cycle on 64
+// dword banks, ds_write_b64 16 lanes on 32, ds_read_b128 16-lane groups mixing two systems.  The
+// full-matrix build scratch (<= 20 row slots) has an EVEN row stride NC + 2: the build's writes of
+// (i, i + d) and (i + d, i) step 2 (MS + 1) dwords per lane, distinct banks for 16 lanes (NC + 1 put
+// lanes i and i + 8 on one bank); the read-back's rows MS doubles apart land on the 16 even double
+// positions mod 32, and the next system starts an ODD number of doubles later, so the two systems of
+// one 32-lane group read disjoint banks.  The half scheme's odd row stride (24 slots) takes 16 of the
+// 32 positions, its complement 16 doubles on.  The eps-scaled coordinates of the next system start
+// 16 bytes (an odd bank quad) further on, so the ds_read_b128 groups' two systems meet no common quad.
+// 32 slots stay as they were: two blocks per CU already take the whole LDS.
+template <int NC>
+constexpr int ns_full_stride() { return PTV_NS_LDS_PAD ? NC + 2 : NC + 1; }
+template <int NC, bool FULL>
+constexpr int ns_sys_stride() {
+    const int base = FULL ? NC * ns_full_stride<NC>() : NC * NsBuild<NC>::HS;
+    if (!PTV_NS_LDS_PAD || (!FULL && !(NsBuild<NC>::HS & 1))) return base;  // pow2 half scheme: LDS-bound, as is
+    const int want = FULL ? 1 : 16;                                          // offset mod 32 doubles
+    return base + ((want - base % 32) + 32) % 32;
+}
+template <int NC>
+constexpr int ns_ye_stride() { return PTV_NS_LDS_PAD && NC <= 24 ? 2 * NC + 1 : 2 * NC; }  // in double2 (16 B); 32 slots: LDS full
+
 // The symmetric build's phi entries: the NC x H (row i, column (i + d) mod NC) entries as one list
 // dealt round-robin over the 16 lanes of a system (ceil(NC H / 16) phi per lane: 13 at 20 slots, 18
 // at 24, where one row per lane-set costs R H = 20, 24), each written where the read-back finds it
@@ -147,7 +172,7 @@ template <int KERN, int NC, bool FULL>
 __device__ __forceinline__ void ns_build(double *__restrict__ ss, const double4 *__restrict__ ye, int li, int k,
                                          const double2 *__restrict__ lt) {
     using Bd = NsBuild<NC>;
-    constexpr int H = Bd::H, MS = NC + 1;
+    constexpr int H = Bd::H, MS = ns_full_stride<NC>();
     constexpr int NSLOT = NC * H;
     constexpr int SPL = (NSLOT + 15) / 16;
     static_assert(NC >= 16, "at most one wrap of the row index per step");
@@ -215,13 +240,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     // NC + 1, odd: conflict-free 16-lane rows and columns; every entry read back with a constant
     // offset, no per-entry address arithmetic), above that the half-matrix scheme of NsBuild
     constexpr bool FULL = NC <= 20;
-    constexpr int MS = NC + 1;
-    constexpr int SCS = FULL ? 4 * NC * MS : 4 * NC * Bd::HS;
+    constexpr int MS = ns_full_stride<NC>();
+    constexpr int SYS = ns_sys_stride<NC, FULL>();
+    constexpr int SCS = 4 * SYS;
     constexpr int SVS = 4 * NC * 8;  // sorted (values, yhat) double4 pairs per wave
     constexpr int SRS = NP * R * 64 + 4 * (2 * NP + 1);  // reflectors (per lane) + tau, beta, pivot tolerance (per system)
     constexpr int SC0 = SCS > SVS ? SCS : SVS;
     constexpr int SC = SC0 > SRS ? SC0 : SRS;
-    __shared__ double4 s_ye[4][4][NC];  // per wave and system: eps-scaled coordinates + id, id order
+    constexpr int YES = ns_ye_stride<NC>();
+    __shared__ double2 s_ye[4][4 * YES];  // per wave and system (YES double2 apart): eps-scaled coordinates + id, id order
     __shared__ double s_sc[4][SC];
     // the log's reduction table: in LDS up to 24 slots (8 KB; two blocks per CU still fit), read
     // from global memory (L1) at 32, where the two blocks' scratch takes the whole LDS
@@ -319,7 +346,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     int lane = threadIdx.x & 63;
     asm volatile("" : "+v"(lane));
     const int seg = lane >> 4, li = lane & 15;
-    double4 *ye = s_ye[wid][seg];
+    double4 *ye = reinterpret_cast<double4 *>(s_ye[wid] + seg * YES);  // 16-B aligned (ds_read_b128 pairs)
     double *sc = s_sc[wid];
     double4 *sv = reinterpret_cast<double4 *>(sc) + seg * NC * 2;  // row r: sv[2r] values, sv[2r+1] yhat
     const long long v = qd * 4 + seg;  // chunk-local voxel
@@ -463,7 +490,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 
     PTV_NS_MARK(2);
     // ---- 3. symmetric build of Phi (NsBuild), read back row by row with y_t = Phi v_t accumulated ----
-    double *ss = sc + seg * (FULL ? NC * MS : NC * Bd::HS);
+    double *ss = sc + seg * SYS;
     if constexpr (FULL) {
 #pragma unroll
         for (int q = 0; q < R; ++q) {
