@@ -102,6 +102,17 @@ constexpr bool tighten_keys() {
     return (MODE == kModeFilter && (PTV_TIGHTEN_KEYS & 1)) || (MODE == kModeInterp && (PTV_TIGHTEN_KEYS & 2));
 }
 constexpr int kCap = 128;        // LDS candidate slots per wave (16 B fp32 + 32 B fp64 each)
+// dev builds: candidate slots and waves per SIMD of the one-slot (k = 1) kernel.  Same-box A/B,
+// 512^3 / 5M nearest: 128 slots at 5 waves 8.42 ms; 96 at 6 (80 VGPRs, 24 spilled) 9.12; 96 at 7
+// 10.06; 80 at 6 9.23 -- the spills cost more than the occupancy gives
+#ifndef PTV_KCAP1
+#define PTV_KCAP1 128
+#endif
+#ifndef PTV_KNN_WAVES_K1
+#define PTV_KNN_WAVES_K1 PTV_KNN_WAVES_SMALL  // dev builds: waves per SIMD of the one-slot kernel
+#endif
+template <int KMAX>
+constexpr int cand_cap() { return KMAX == 1 ? PTV_KCAP1 : kCap; }
 constexpr int kRowsPerLane = 1;  // cell rows examined per lane per gather round
 constexpr int kRunEntries = 64 * 2 * kRowsPerLane;  // x-runs per gather round (power of two)
 
@@ -750,6 +761,7 @@ constexpr bool kKeyList = KMAX >= 16 && !EXACT;
 
 template <int KMAX, int MODE, bool EXACT>
 constexpr int knn_waves() {
+    if (KMAX == 1) return PTV_KNN_WAVES_K1;
     if (KMAX <= 4) return PTV_KNN_WAVES_SMALL;
     if (KMAX <= 8) return PTV_KNN_WAVES;
     // key lists: the search fits 3 waves per SIMD up to 32 slots, the streamed interpolation
@@ -777,6 +789,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
         }
     };
     if constexpr (STAMP) t_mark = __builtin_amdgcn_s_memtime();
+    constexpr int kCap = cand_cap<KMAX>();
     __shared__ double4 lds_cand[4][kCap];
     __shared__ __attribute__((aligned(16))) float lds_cfx[4][kCap], lds_cfy[4][kCap], lds_cfz[4][kCap];
     __shared__ uint2 lds_runs[4][kRunEntries];
@@ -970,7 +983,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                 uint32_t *tab = reinterpret_cast<uint32_t *>(buf);
                 const uint32_t sl = __float_as_uint(seed.w);
                 const bool has = sl != 0xffffffffu;
-                const uint32_t hsh = (sl * 2654435761u) >> 22;  // 1024 entries = the 4 KB buffer
+                // 1024 entries = the 4 KB buffer (512 in a smaller one-slot buffer)
+                const uint32_t hsh = (sl * 2654435761u) >> (kCap >= 128 ? 22 : 23);
                 if (has) tab[hsh] = (uint32_t)lane;
                 wave_lds_sync();
                 const bool uniq = has && tab[hsh] == (uint32_t)lane;
