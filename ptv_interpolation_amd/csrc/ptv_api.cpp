@@ -523,6 +523,15 @@ int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchP
                        c->pval.p, s));
     PTV_HIP(hipEventRecord(c->ev_bin1, s));
 
+    // Seed records for the main launch (the finest level's k-NN lists) pay for the pair lists (k <=
+    // 12): headline 22.4 -> 14.1 ms with them, k = 12 33.2 -> 29.4 ms.  For the packed-key lists (k >=
+    // 13) the union-seed counting costs more than its tighter bound saves, and the finest level then
+    // writes no records either (1.7 GB per launch at k = 50).  Same-box A/B, 512^3 / 5M, main launch
+    // + lattice without / with them: k = 16 34.8 + 2.14 / 35.9 + 2.23 ms, Sibson k = 30 54.1 + 2.71 /
+    // 55.2 + 2.84, IDW k = 50 102.3 + 5.13 / 104.2 + 5.40, Sibson k = 50 137.9 + 5.09 / 138.8 +
+    // 5.38, RBF slot searches k = 20 29.0 / 29.9 and C3 48.4 / 50.0.
+    bool main_seeds = kmax_for(prm->k) <= 12;
+    if (const char *e = dev_knob("PTV_MAIN_SEEDS")) main_seeds = e[0] == '1';  // dev knob: 1 = always, 0 = never
     // 3. coarse-lattice k-th distance bounds (separable grids): every 4th point of the
     //    grid, recursively, down to a few tens of thousands of points; each level is an
     //    exact k-NN pass (k-th distance only) bounded by the next coarser level.
@@ -590,7 +599,7 @@ int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchP
         // seed records (each lattice point's k-NN, 16 B each) for the next finer level's tiles,
         // unless they would take more than kSeedBytesMax (then the D(c) + |v - c| bound alone)
         const size_t nrec = (size_t)lat[l].n[0] * lat[l].n[1] * lat[l].n[2] * prm->k;
-        if (nrec * sizeof(float4) <= kSeedBytesMax) {
+        if ((l > 0 || main_seeds) && nrec * sizeof(float4) <= kSeedBytesMax) {
             PTV_TRY(c->lat_recs[l].ensure(nrec));
             lat[l].recs = c->lat_recs[l].p;
         }
@@ -655,7 +664,7 @@ int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchP
         kl.cb.ay = lat[0].ay;
         kl.cb.az = lat[0].az;
         kl.cb.dk = lat[0].dk;
-        kl.cb.recs = lat[0].recs;
+        kl.cb.recs = lat[0].recs;  // NULL unless main_seeds
         for (int d = 0; d < 3; ++d) kl.cb.n[d] = lat[0].n[d];
     }
     PTV_HIP(hipEventRecord(c->ev_lat1, s));
