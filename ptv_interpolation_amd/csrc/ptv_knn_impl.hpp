@@ -69,13 +69,17 @@ namespace ptv {
 
 #ifndef PTV_KNN_UNROLL_MAX
 // key-list interpolation epilogues up to this many slots unroll their blocks at compile time;
-// longer lists run the rolled passes
-#define PTV_KNN_UNROLL_MAX 32
+// longer lists run the rolled passes.  Round 5: 32 -> 56 (with KEEP below; the key list's 2 x KMAX
+// VGPRs are dead by the epilogue, so the kept distances fit the 2-wave budget: 8 VGPRs spilled at
+// 56 slots).  Same-box A/B, 512^3 / 5M main launch: Sibson k = 45 119.6 -> 87.9 ms, Sibson k = 50
+// 137.2 -> 100.0, IDW k = 36 77.7 -> 75.4, IDW k = 50 101.8 -> 100.8.  At 64 slots Sibson k = 60
+// gains (160.9 -> 126.5) but IDW k = 60 loses (122.1 -> 130.2, 49 VGPRs spilled): 64 stays rolled.
+#define PTV_KNN_UNROLL_MAX 56
 #endif
 #ifndef PTV_KNN_KEEP_MAX
 // key lists up to this many slots keep the epilogue's distances (then weights) in registers
-// between passes; longer ones re-gather the records every pass
-#define PTV_KNN_KEEP_MAX 32
+// between passes; longer ones re-gather the records every pass (Sibson: four passes)
+#define PTV_KNN_KEEP_MAX 56
 #endif
 #ifndef PTV_STAMP_SEEDSPLIT
 #define PTV_STAMP_SEEDSPLIT 0  // dev stamp builds: union-seed counting passes stamped as 'setup'
@@ -1892,8 +1896,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
         return;
     }
     if constexpr (KSL && MODE == kModeInterp && KMAX <= PTV_KNN_UNROLL_MAX) {
-        // up to 32 slots: blocks unrolled at compile time (the loads of different blocks overlap,
-        // measured faster than the rolled loop below at 3 waves per SIMD: Sibson k = 30 79 vs 92 ms)
+        // up to PTV_KNN_UNROLL_MAX (56) slots: blocks unrolled at compile time (the loads of different
+        // blocks overlap, measured faster than the rolled loop below: Sibson k = 30 79 vs 92 ms at 3
+        // waves per SIMD, Sibson k = 50 100 vs 137 ms at 2)
         // Key lists (k >= 13): the weights are streamed in blocks of 8 neighbours from the exact
         // d2, recomputed from the records (the keys hold truncated d2), in the reference's order:
         // interpolator.py:142-153 (IDW), :102-122 (Sibson).  Register-kept distances where the
