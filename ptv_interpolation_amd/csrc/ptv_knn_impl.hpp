@@ -1055,7 +1055,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                 stamp(t_seed);
             }
         }
-        if constexpr (KMAX > 8) {
+        // (the launcher gives the key-list interpolation and slot launches no seed records: the
+        // union-seed code is not compiled into them, which frees its registers)
+        if constexpr (KMAX > 8 && !(KEYS && (MODE == kModeInterp || MODE == kModeSlots))) {
             if (a.cb.recs != nullptr) {
                 // ---- seeds (k > 8): the union of the 8 corners' k-NN lists bounds every voxel's
                 //      k-th distance (measured: within 0.03 % of it in volume, the D(c) + |v - c|
