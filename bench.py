@@ -36,7 +36,7 @@ padded to the largest one when they differ) is timed once after it and reported 
   on one GPU.
 
 ``--share R/N`` (one GPU, no collective) runs rank R's step of the N-rank strong partition:
-the per-rank step time a rehearsal of the N-GPU run is built from (tools/gpu_scaling.sh).
+the per-rank step time a rehearsal of the N-GPU run is built from (tools/share_balance.py).
 ``--dry-run`` (CPU, gloo) runs the launcher and the partition / broadcast / padded all-gather
 with a plane-index fill in place of the kernel (tests/test_bench_launch.py).
 
