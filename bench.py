@@ -684,8 +684,19 @@ def main_interp(args):
                 mask_t = _device_fluid_mask(G, nz, (za, zb), dev)
                 fluid_frac = float(mask_t[z0:z1].float().mean().item())
 
+    cold = None
     for w in range(args.warmup):
+        if w == 0:
+            # the cold call (a one-shot interpolate_field: no cached cull map, every particle binned)
+            torch.cuda.synchronize(dev)
+            tc = time.perf_counter()
         step()
+        if w == 0:
+            torch.cuda.synchronize(dev)
+            st0 = ctx.last_stats()
+            cold = {"wall_ms": round((time.perf_counter() - tc) * 1e3, 3),
+                    "device_ms": round(st0["ms_bin"] + st0["ms_cull"] + st0["ms_lattice"] + st0["ms_knn"] +
+                                       st0["ms_solve"], 3), "n_binned": int(st0["n_binned"])}
         if balance and w in (1, 3) and w + 1 < args.warmup:
             rebalance()
     torch.cuda.synchronize(dev)
@@ -765,7 +776,9 @@ def main_interp(args):
         ach = alg / (avg["ms_knn"] * 1e-3) / 1e9
         t_step = avg["ms_bin"] + avg["ms_cull"] + avg["ms_lattice"] + avg["ms_knn"]
         alg_step = alg + 48 * avg["n_binned"]
-        headline_shape = (G == 512 and args.particles == 5_000_000 and k == 8 and not args.mask and not out_f32)
+        # the committed PMC traffic is the whole-grid one-GPU launch's: never a share's or a slab's
+        headline_shape = (G == 512 and args.particles == 5_000_000 and k == 8 and not args.mask and not out_f32
+                          and world == 1 and share is None and not radius)
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBPS, 4),
                 "traffic": traffic_from_profiles()[0] if headline_shape else None,
@@ -800,9 +813,12 @@ def main_interp(args):
             wl = (f"{G}x{G}x{nz} grid = {world} stacked {G}^3 sphere-pack copies / {args.particles * world} "
                   f"particles (replicated), {G}^3 slab + {args.particles} particles' copy per GPU")
         else:
-            wl = f"{G}^3 grid / {args.particles} particles (replicated), z-slab of {G // world if world else G} planes per GPU"
+            sizes = [bounds[r + 1] - bounds[r] for r in range(world)] if bounds is not None else [G]
+            per = (f"{sizes[0]} planes" if min(sizes) == max(sizes) else f"{min(sizes)}-{max(sizes)} planes")
+            wl = f"{G}^3 grid / {args.particles} particles (replicated), z-slabs of {per} per GPU"
         if share is not None:
-            wl = f"rank {rank} of {world}: planes [{z0}, {z1}) of the " + wl + " (one-GPU rehearsal, no collective)"
+            wl = (f"rank {rank} of {world}: planes [{z0}, {z1}) ({z1 - z0} planes) of the " + wl +
+                  " (one-GPU rehearsal, no collective)")
         if rbf:
             wl += f"; local RBF {kern} k={k} eps={eps} degree={deg} (system {m_sys}) fp64"
         else:
@@ -832,6 +848,10 @@ def main_interp(args):
         }
         if share is not None:
             line["share"] = {"rank": rank, "world": world}
+        if cold is not None:
+            line["cold_call"] = dict(cold, note="first warmup step on a fresh context (includes one-time "
+                                                "buffer allocation; N > 1: no cached cull map, every "
+                                                "particle binned; before any re-cut)")
         if args.mask:
             line["fluid_mvoxels_per_s"] = round(value * fluid_frac, 2)
         if bounds is not None and world > 1:

@@ -74,6 +74,7 @@ struct ptv_ctx {
     DevBuf<double> lat_axes[kMaxLattice], lat_dk[kMaxLattice];  // coarse-lattice bound levels
     DevBuf<float4> lat_recs[kMaxLattice];                        // their k-NN records (seeds, fp32 relative)
     DevBuf<int> lat_order[kMaxLattice];                          // longest-first block order per level
+    DevBuf<double> lat_okeys;                                    // its block keys (scratch)
     DevBuf<uint32_t> lat_split;                                  // split lattice launch: partial lists
     // PTV_FLAG_SLAB_CULL_AUTO: the cached per-column cull map (top, bot), its key, the proof's
     // need map and scratch
@@ -230,6 +231,7 @@ int ptv_free(ptv_ctx *c) {
     for (auto &b : c->lat_dk) b.release();
     for (auto &b : c->lat_recs) b.release();
     for (auto &b : c->lat_order) b.release();
+    c->lat_okeys.release();
     c->lat_split.release();
     for (auto &b : c->cmap) b.release();
     c->cdk.release();
@@ -323,6 +325,10 @@ constexpr size_t kSeedBytesMax = 40ULL << 30;    // lattice seed records per lev
 constexpr int kLatticeSplit = 16;
 constexpr long long kLatticeSplitMinBlocks = 64;
 constexpr long long kLatticeSplitDiv = 128;
+// cap on the split launch's partial-list buffer (split_blocks * 4 * kLatticeSplit * KMAX * 64 slots,
+// memset once per level): 64 MiB = 512 blocks at KMAX 8, 32 at 128; the measured win came from the
+// first ~64 blocks, while nb / 128 at 2048^3 would be ~4300 blocks (0.56 GB at k = 8, 9 GB at 127)
+constexpr size_t kLatticeSplitBytesMax = 64ULL << 20;
 // relative widening of the cached slab cull map over the need it was built from
 constexpr double kCullMapSlack = 1e-6;
 
@@ -378,7 +384,7 @@ int validate_knn(const ptv_particles *p, const ptv_knn_params *prm) {
         return PTV_E_ARG;
     }
     if (kmax_for(prm->k) == 0) {
-        set_error("k=" + std::to_string(prm->k) + " exceeds the GPU k-NN list limit (64)");
+        set_error("k=" + std::to_string(prm->k) + " exceeds the GPU k-NN list limit (127; 126 for the outlier filter)");
         return PTV_E_UNSUPPORTED;
     }
     return PTV_OK;
@@ -613,8 +619,9 @@ int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchP
             const long long nb = (long long)(((lat[l].n[0] + 3) / 4 + 3) / 4) * ((lat[l].n[1] + 3) / 4) *
                                  ((lat[l].n[2] + 3) / 4);
             PTV_TRY(c->lat_order[l].ensure((size_t)nb));
+            PTV_TRY(c->lat_okeys.ensure((size_t)nb + 1));
             PTV_TRY(launch_block_order(lat[l + 1].dk, lat[l + 1].n, lat[l].n[0], lat[l].n[1], lat[l].n[2], kl.r0,
-                                       c->lat_order[l].p, s));
+                                       c->lat_order[l].p, c->lat_okeys.p, s));
             ll.order = c->lat_order[l].p;
             if (const char *e = dev_knob("PTV_DBG_ORDER")) {  // dev builds: the order and the coarser bounds
                 if (l == 0) {
@@ -637,6 +644,9 @@ int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchP
             long long sblk = std::min<long long>(nb, std::max<long long>(kLatticeSplitMinBlocks, nb / kLatticeSplitDiv));
             if (const char *e = dev_knob("PTV_LAT_SPLIT")) split = std::atoi(e);          // dev: 0 = off
             if (const char *e = dev_knob("PTV_LAT_SPLIT_BLOCKS")) sblk = std::min<long long>(nb, std::atoll(e));
+            if (split > 1)
+                sblk = std::min<long long>(sblk, (long long)(kLatticeSplitBytesMax / sizeof(uint32_t) /
+                                                             kdist_split_slots(split, 1, kmax_for(prm->k))));
             if (split > 1 && sblk > 0) {
                 PTV_TRY(c->lat_split.ensure(kdist_split_slots(split, (int)sblk, kmax_for(prm->k))));
                 ll.split = split;
@@ -737,7 +747,8 @@ SearchParams knn_search(const ptv_knn_params *prm) {
 // whose key matches the cached map culls with it and proves the cull on the device (the need map
 // of the kept particles' lattice inside the used map everywhere) before the gated main launch; a
 // call without a cached map (or whose proof fails) bins every particle and builds the map from its
-// own lattice.  Key: the particle arrays, n, a 96-value fingerprint, the grid, the slab, k, method.
+// own lattice.  Key: the particle arrays, n, a 96-value fingerprint, the axis values, the grid, the
+// slab, k, method.
 int run_knn_auto(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn_params *prm,
                  const double *ax, const double *ay, const double *az, const uint8_t *mask, double *U, double *V,
                  double *W, hipStream_t s, ptv_stats *st) {
@@ -747,8 +758,16 @@ int run_knn_auto(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const pt
     PTV_TRY(c->cfp.ensure(6 * kFingerprint));
     PTV_TRY(launch_fingerprint(src, n, c->cfp.p, s));
     std::vector<double> &key = c->ckey_new;
-    key.assign(6 * kFingerprint, 0.0);
-    PTV_HIP(hipMemcpyAsync(key.data(), c->cfp.p, 6 * kFingerprint * sizeof(double), hipMemcpyDeviceToHost, s));
+    // the fingerprint, then the grid's axis values: the map and the cached lattice bounds belong to
+    // lattice positions, and a reused axis buffer (the host path's c->axes, a recycled torch
+    // allocation) can hold other coordinates under the same pointer
+    const size_t nfp = 6 * kFingerprint;
+    key.assign(nfp + (size_t)(g->nx + g->ny + g->nz), 0.0);
+    PTV_HIP(hipMemcpyAsync(key.data(), c->cfp.p, nfp * sizeof(double), hipMemcpyDeviceToHost, s));
+    PTV_HIP(hipMemcpyAsync(key.data() + nfp, ax, (size_t)g->nx * sizeof(double), hipMemcpyDefault, s));
+    PTV_HIP(hipMemcpyAsync(key.data() + nfp + g->nx, ay, (size_t)g->ny * sizeof(double), hipMemcpyDefault, s));
+    PTV_HIP(hipMemcpyAsync(key.data() + nfp + g->nx + g->ny, az, (size_t)g->nz * sizeof(double), hipMemcpyDefault,
+                           s));
     PTV_HIP(hipStreamSynchronize(s));
     for (const void *q : {(const void *)p->x, (const void *)p->y, (const void *)p->z, (const void *)p->u,
                           (const void *)p->v, (const void *)p->w, (const void *)ax, (const void *)ay,
@@ -1106,12 +1125,13 @@ int run_rbf(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_rbf
     ra.smoothing = prm->smoothing;
     ra.flags = prm->flags;
     int st_out[6] = {0, 0, 0, 0, 0, 0};
-    // per chunk: the voxels k_rbf_ns flagged (status[3] of its launch) and whether they overflowed
-    // the list (status[4]), copied on the device after each chunk
-    PTV_TRY(c->rbf_cflag.ensure(2 * (size_t)nchunks));
-    std::vector<int> cflag(2 * (size_t)nchunks, 0);
+    // per chunk: the voxels k_rbf_ns flagged (status[3] of its launch), whether they overflowed the
+    // list (status[4]) and the running singular count (status[0]), copied on the device after each chunk
+    PTV_TRY(c->rbf_cflag.ensure(3 * (size_t)nchunks));
+    std::vector<int> cflag(3 * (size_t)nchunks, 0);
     std::vector<char> rerun((size_t)nchunks, 1);
     int64_t pivoted = 0;
+    int64_t singular_redone = 0;  // pass 0's singular counts of the chunks an overflow rerun solves again
     for (int pass = 0; pass < 2; ++pass) {
     // pass 1 (rare): k_rbf_spd16 met a pivot its reciprocal does not serve (every chunk again with the
     // LDS-broadcast SPD kernel: the same arithmetic plus the IEEE division for such pivots), or
@@ -1139,7 +1159,9 @@ int run_rbf(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_rbf
         PTV_TRY(launch_rbf(ra, b, c->slots.p, ax, ay, az, qx, qy, qz, smooth, c->rbf_pw.p, mask, U, V, W,
                            c->rbf_status.p, s));
         if (pass == 0) {
-            PTV_HIP(hipMemcpyAsync(c->rbf_cflag.p + 2 * ch, c->rbf_status.p + 3, 2 * sizeof(int),
+            PTV_HIP(hipMemcpyAsync(c->rbf_cflag.p + 3 * ch, c->rbf_status.p + 3, 2 * sizeof(int),
+                                   hipMemcpyDeviceToDevice, s));
+            PTV_HIP(hipMemcpyAsync(c->rbf_cflag.p + 3 * ch + 2, c->rbf_status.p, sizeof(int),
                                    hipMemcpyDeviceToDevice, s));
             PTV_HIP(hipMemsetAsync(c->rbf_status.p + 4, 0, sizeof(int), s));
         }
@@ -1149,15 +1171,19 @@ int run_rbf(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_rbf
     if (pass == 0)
         PTV_HIP(hipMemcpyAsync(cflag.data(), c->rbf_cflag.p, cflag.size() * sizeof(int), hipMemcpyDeviceToHost, s));
     PTV_HIP(hipStreamSynchronize(s));
-    if (pass == 1) break;
+    if (pass == 1) {
+        st_out[0] -= (int)singular_redone;  // each rerun chunk's singular voxels, counted once
+        break;
+    }
     bool again = false;
     for (int ch = 0; ch < nchunks; ++ch) {
         const int za = (int)(z0 + (int64_t)ch * cp), zb = (int)std::min<int64_t>(z1, za + cp);
-        const bool over = cflag[2 * ch + 1] != 0;
+        const bool over = cflag[3 * ch + 1] != 0;
         // voxels the pivoting kernel solved: the flagged ones, or every voxel of an overflowed chunk
-        pivoted += over ? (int64_t)(zb - za) * plane : cflag[2 * ch];
+        pivoted += over ? (int64_t)(zb - za) * plane : cflag[3 * ch];
         rerun[ch] = (st_out[2] != 0 || over) ? 1 : 0;
         again = again || rerun[ch];
+        if (over && st_out[2] == 0) singular_redone += cflag[3 * ch + 2] - (ch > 0 ? cflag[3 * ch - 1] : 0);
     }
     if (st_out[2] != 0) pivoted = 0;  // the SPD rerun: no null-space kernel ran
     if (!again) break;

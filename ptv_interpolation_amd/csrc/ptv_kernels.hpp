@@ -134,7 +134,7 @@ inline size_t kdist_split_slots(int split, int split_blocks, int kmax) {
 // coarser points around it (D / unit, 256 buckets), and `order` lists the blocks by descending
 // key, so the void tiles (long searches) start first instead of forming the launch's tail.
 int launch_block_order(const double *dk_coarse, const int nc[3], int nx, int ny, int nz, double unit, int *order,
-                       hipStream_t s);
+                       double *keys, hipStream_t s);  // keys: nblocks + 1 doubles of scratch
 
 // Upper bound on the k-th neighbour distance of every point of a separable grid by
 // counting the particles of cells entirely inside balls around it (coarsest lattice).

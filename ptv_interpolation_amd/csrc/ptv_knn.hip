@@ -146,41 +146,43 @@ int launch_halo_need(const double *lax, const double *lay, const double *laz, in
 }
 
 // ---------------------------------------------------------------------------
-// Longest-first block order of a lattice-level launch (one workgroup of 1024 threads: a
-// bucket histogram of the block keys in LDS, a scan, then placement by LDS atomics; the
-// order inside a bucket is arbitrary, which changes nothing but the dispatch order).
+// Longest-first block order of a lattice-level launch.  k_block_keys (one thread per block,
+// many workgroups) computes each block's key once, and their maximum; k_block_order (one
+// workgroup of 1024 threads) buckets the keys in LDS, scans, and places the blocks by LDS atomics
+// (the order inside a bucket is arbitrary, which changes nothing but the dispatch order).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_block_order(const double *__restrict__ dkc, int cnx, int cny, int cnz,
-                                                      int ntxb, int nty, int nblocks, double inv_unit,
-                                                      int *__restrict__ order) {
-    __shared__ int cnt[256];
-    __shared__ int base[256];
-    __shared__ double dmx[1024];
-    auto key = [&](int b) -> double {
+__global__ __launch_bounds__(256) void k_block_keys(const double *__restrict__ dkc, int cnx, int cny, int cnz,
+                                                    int ntxb, int nty, int nblocks, double *__restrict__ keys,
+                                                    unsigned long long *__restrict__ kmax) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    double D = 0.0;
+    if (b < nblocks) {
         // block b: tiles (bx*4 .. bx*4+3, ty, tz) = points x [16 bx, 16 bx + 15], y [4 ty, 4 ty + 3],
         // z [4 tz, 4 tz + 3]; coarser point j sits at point 4 j (kLatticeStep), so the block lies in
         // the coarser cells spanned by x [4 bx, 4 bx + 4], y [ty, ty + 1], z [tz, tz + 1]
         const int bx = b % ntxb, rr = b / ntxb, ty = rr % nty, tz = rr / nty;
-        double D = 0.0;
         for (int z = tz; z <= tz + 1; ++z)
             for (int y = ty; y <= ty + 1; ++y)
                 for (int x = 4 * bx; x <= 4 * bx + 4; ++x)
                     D = fmax(D, dkc[((size_t)min(z, cnz - 1) * cny + min(y, cny - 1)) * cnx + min(x, cnx - 1)]);
-        return D;
-    };
+        keys[b] = D;
+    }
+    // non-negative doubles (and +inf) order as their bit patterns
+    const double m = group_reduce<0x3f>(D, OpMax{});
+    if ((threadIdx.x & 63) == 0) atomicMax(kmax, (unsigned long long)__double_as_longlong(m));
+}
+
+__global__ __launch_bounds__(1024) void k_block_order(const double *__restrict__ keys,
+                                                      const unsigned long long *__restrict__ kmax, int nblocks,
+                                                      double inv_unit, int *__restrict__ order) {
+    __shared__ int cnt[256];
+    __shared__ int base[256];
     // buckets of the largest key / 256 (a fixed unit saturated: at 512^3 every block near a sphere
     // centre fell into the top bucket, in arbitrary order, and the slowest void tile could start last)
-    double m = 0.0;
-    for (int b = threadIdx.x; b < nblocks; b += blockDim.x) m = fmax(m, key(b));
-    dmx[threadIdx.x] = m;
-    __syncthreads();
-    for (int st = 512; st > 0; st >>= 1) {
-        if ((int)threadIdx.x < st) dmx[threadIdx.x] = fmax(dmx[threadIdx.x], dmx[threadIdx.x + st]);
-        __syncthreads();
-    }
-    const double scale = dmx[0] > 0.0 && dmx[0] < INFINITY ? 255.99 / dmx[0] : inv_unit;
+    const double mx = __longlong_as_double((long long)*kmax);
+    const double scale = mx > 0.0 && mx < INFINITY ? 255.99 / mx : inv_unit;
     auto bucket = [&](int b) -> int {
-        const double q = key(b) * scale;
+        const double q = keys[b] * scale;
         return 255 - (q < 255.0 ? (int)q : 255);  // descending bound -> ascending bucket
     };
     for (int i = threadIdx.x; i < 256; i += blockDim.x) cnt[i] = 0;
@@ -199,15 +201,20 @@ __global__ __launch_bounds__(1024) void k_block_order(const double *__restrict__
 }
 
 int launch_block_order(const double *dk_coarse, const int nc[3], int nx, int ny, int nz, double unit, int *order,
-                       hipStream_t s) {
+                       double *keys, hipStream_t s) {
     const int ntxb = ((nx + 3) / 4 + 3) / 4, nty = (ny + 3) / 4, ntz = (nz + 3) / 4;
     const long long nblocks = (long long)ntxb * nty * ntz;
     if (nblocks > 0x7fffffffLL || !(unit > 0.0)) {
         set_error("lattice block order: bad launch shape");
         return PTV_E_ARG;
     }
-    hipLaunchKernelGGL(k_block_order, dim3(1), dim3(1024), 0, s, dk_coarse, nc[0], nc[1], nc[2], ntxb, nty,
-                       (int)nblocks, 8.0 / unit, order);
+    // keys[nblocks] holds the maximum's bits
+    unsigned long long *kmax = reinterpret_cast<unsigned long long *>(keys + nblocks);
+    PTV_HIP(hipMemsetAsync(kmax, 0, sizeof(unsigned long long), s));
+    hipLaunchKernelGGL(k_block_keys, dim3((unsigned)((nblocks + 255) / 256)), dim3(256), 0, s, dk_coarse, nc[0],
+                       nc[1], nc[2], ntxb, nty, (int)nblocks, keys, kmax);
+    PTV_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_block_order, dim3(1), dim3(1024), 0, s, keys, kmax, (int)nblocks, 8.0 / unit, order);
     PTV_HIP(hipGetLastError());
     return PTV_OK;
 }

@@ -275,7 +275,8 @@ def _knn_field(points, values, grid_tuple, method, k, power, radius=0.0):
             return dict(ctx.stats)
 
         full = [np.empty((nz, len(axes[1]), len(axes[0]))) for _ in range(3)]
-        U, V, W = launcher.run_slabs(nz, slab, full)
+        # later calls on this grid re-cut the slabs from these slabs' measured device times
+        U, V, W = launcher.run_slabs(nz, slab, full, balance_key=("knn", m, k) if flags else None)
     else:
         ctx = _lib.Context.get(launcher.devices()[0])
         size = int(np.prod(shape))

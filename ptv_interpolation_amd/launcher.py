@@ -12,11 +12,21 @@ calls); no collective touches the data path.
 
 Devices: ``PTV_DEVICE=i`` pins one device; ``PTV_DEVICES=0,1,...`` lists them (a device
 may repeat: several contexts, one per slab, on the same GPU); default all visible GPUs.
+
+Slab bounds start even; callers that pass a ``balance_key`` (the k-NN methods) get them re-cut
+from the slabs' measured device times (``zslab.balanced_bounds``, as bench.py's warmup does), at
+most ``MAX_RECUTS`` times per (grid, devices, key), and only from calls whose slabs all ran culled
+(a cold call's time is dominated by binning every particle, not by its planes).  A re-cut changes
+the slabs' keys, so the next call of each slab builds its cull map again.
+
+Each context is used by one thread at a time (a per-context lock held across ``fn``): concurrent
+calls share the slab contexts, their buffers and their cached cull maps.
 """
 from __future__ import annotations
 
 import os
 import threading
+import time
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
@@ -25,6 +35,9 @@ from . import _lib
 
 _ctx_lock = threading.Lock()
 _slab_ctx = {}
+_use_locks = {}  # id(context) -> lock held while a slab runs on it
+_balance = {}  # (nz, devices, balance_key) -> {"bounds": [...], "recuts": int}
+MAX_RECUTS = 2
 _tls = threading.local()  # per calling thread: what fn returned for each slab of its last run_slabs
 
 
@@ -63,37 +76,91 @@ def context(device: int, slot: int) -> "_lib.Context":
     return c
 
 
-def run_slabs(nz: int, fn, out, results=None):
+def _use_lock(ctx):
+    with _ctx_lock:
+        lk = _use_locks.get(id(ctx))
+        if lk is None:
+            lk = _use_locks[id(ctx)] = threading.Lock()
+    return lk
+
+
+def _slab_cost(res, wall_ms):
+    """A slab's cost for the re-cut: its device time when fn returned the call's stats, else wall."""
+    if isinstance(res, dict) and all(k in res for k in ("ms_bin", "ms_cull", "ms_lattice", "ms_knn")):
+        return res["ms_bin"] + res["ms_cull"] + res["ms_lattice"] + res["ms_knn"]
+    return wall_ms
+
+
+def _all_culled(res):
+    return all(isinstance(r, dict) and 0 < r.get("n_binned", 0) < r.get("n_particles", 0) for r in res)
+
+
+def current_bounds(nz: int, parts: int, balance_key=None, devs=None):
+    """The N + 1 slab boundaries run_slabs uses for this grid (balanced ones once measured)."""
+    even = [0] + [b for _, b in slab_bounds(nz, parts)]
+    if balance_key is None:
+        return even
+    ent = _balance.get((nz, tuple(devs if devs is not None else devices()), balance_key))
+    return list(ent["bounds"]) if ent is not None and len(ent["bounds"]) == len(even) else even
+
+
+def run_slabs(nz: int, fn, out, results=None, balance_key=None):
     """Fill the preallocated C-contiguous (nz, ...) arrays ``out`` slab by slab.
 
     ``fn(ctx, z0, z1, views)`` writes planes [z0, z1) into ``views`` (the z-slices of ``out``,
     contiguous, written in place by the library's D2H: no per-slab arrays and no host
     concatenation).  One slab per device of ``devices()``, one host thread each; a single
     device runs fn(ctx, 0, nz, out) directly.  Returns ``out``; fn's per-slab results are
-    ``last_results`` of the calling thread (or appended to ``results`` when given)."""
+    ``last_results`` of the calling thread (or appended to ``results`` when given).
+    ``balance_key``: re-cut the bounds of later calls with the same key from this call's slab
+    costs (see the module docstring)."""
     out = tuple(out)
     for a in out:
         if not (a.flags.c_contiguous and a.shape[0] == nz):
             raise ValueError("run_slabs: outputs must be C-contiguous with nz leading planes")
     devs = devices()
     if len(devs) <= 1 or nz < 2:
-        res = [fn(_lib.Context.get(devs[0]), 0, nz, out)]
+        ctx = _lib.Context.get(devs[0])
+        with _use_lock(ctx):
+            res = [fn(ctx, 0, nz, out)]
         _tls.results = res
         if results is not None:
             results.extend(res)
         return out
-    slabs = slab_bounds(nz, len(devs))
+    parts = min(len(devs), nz)
+    bounds = current_bounds(nz, parts, balance_key, devs)
     seen = {}
     jobs = []
-    for d, (z0, z1) in zip(devs, slabs):
+    for i, d in enumerate(devs[:parts]):
+        z0, z1 = bounds[i], bounds[i + 1]
         slot = seen.get(d, 0)
         seen[d] = slot + 1
         jobs.append((context(d, slot), z0, z1, tuple(a[z0:z1] for a in out)))
+
+    def run(job):
+        with _use_lock(job[0]):
+            t0 = time.perf_counter()
+            r = fn(*job)
+            return r, (time.perf_counter() - t0) * 1e3
+
     with ThreadPoolExecutor(len(jobs)) as ex:
-        res = list(ex.map(lambda j: fn(*j), jobs))
+        timed = list(ex.map(run, jobs))
+    res = [r for r, _ in timed]
     _tls.results = res
     if results is not None:
         results.extend(res)
+    if balance_key is not None and _all_culled(res):
+        key = (nz, tuple(devs), balance_key)
+        ent = _balance.setdefault(key, {"bounds": bounds, "recuts": 0})
+        if ent["recuts"] < MAX_RECUTS:
+            from .zslab import balanced_bounds
+
+            costs = [_slab_cost(r, w) for r, w in timed]
+            if max(costs) > 1.1 * min(costs):
+                new = balanced_bounds(bounds, costs, min_planes=min(12, nz // parts))
+                if new != bounds:
+                    ent["bounds"] = new
+                    ent["recuts"] += 1
     return out
 
 

@@ -103,3 +103,61 @@ def test_slab_cull_map_refreshes_when_particles_change(monkeypatch):
         assert np.array_equal(a, b, equal_nan=True)
     for a, b in zip(three3, one3):
         assert np.array_equal(a, b, equal_nan=True)
+
+
+@pytest.mark.parametrize("change", ["shift", "scale"])
+def test_slab_cull_map_keyed_by_axis_values(change):
+    """The cull map's cache key holds the axis values, not only their pointers: the same particles,
+    the same grid shape and the same axis buffers refilled in place with other coordinates (a
+    recycled allocation) must not reuse the map built for the old lattice positions.  Three slabs,
+    each a cold and a warm call on the old axes, then a call on the new ones; every slab equals the
+    whole-grid call on the same axes bit for bit."""
+    import torch
+
+    from ptv_interpolation_amd import _lib, synth
+
+    G, N = 96, 150_000
+    P, Q = synth.sphere_pack(N, G, values="normal")
+    cols = [torch.from_numpy(np.ascontiguousarray(P[:, i])).cuda() for i in range(3)] + \
+           [torch.from_numpy(np.ascontiguousarray(Q[:, i])).cuda() for i in range(3)]
+    ptrs = [c.data_ptr() for c in cols]
+    axes = [torch.linspace(0, G - 1, G, dtype=torch.float64, device="cuda") for _ in range(3)]
+    aptrs = [a.data_ptr() for a in axes]
+    new = [a * 0.8 + 9.5 if change == "shift" else a * 0.55 for a in axes]
+
+    def whole():
+        ctx = _lib.Context(0)
+        out = [torch.empty((G, G, G), dtype=torch.float64, device="cuda") for _ in range(3)]
+        ctx.interp_knn_dev(N, ptrs, G, G, G, axes_ptrs=aptrs, out_ptrs=[o.data_ptr() for o in out], k=8)
+        torch.cuda.synchronize()
+        ctx.close()
+        return out
+
+    ref_old = whole()
+    slabs = [(0, 30), (30, 61), (61, G)]
+    ctxs = [_lib.Context(0) for _ in slabs]
+    binned = []
+    try:
+        for phase in ("cold", "warm", "new axes"):
+            if phase == "new axes":
+                for a, b in zip(axes, new):
+                    a.copy_(b)
+                torch.cuda.synchronize()
+                ref = whole()
+            else:
+                ref = ref_old
+            for ctx, (z0, z1) in zip(ctxs, slabs):
+                out = [torch.full((z1 - z0, G, G), -7.0, dtype=torch.float64, device="cuda") for _ in range(3)]
+                torch.cuda.synchronize()
+                ctx.interp_knn_dev(N, ptrs, G, G, G, axes_ptrs=aptrs, out_ptrs=[o.data_ptr() for o in out], k=8,
+                                   flags=_lib.FLAG_SLAB_CULL_AUTO, z_range=(z0, z1))
+                torch.cuda.synchronize()
+                binned.append((phase, z0, ctx.last_stats()["n_binned"]))
+                for a, b in zip(out, ref):
+                    assert torch.equal(a, b[z0:z1]), (phase, z0, z1)
+    finally:
+        for c in ctxs:
+            c.close()
+    print(f"{change}: binned per (phase, slab) {binned}")
+    # the new-axes call found no map for its key: every particle binned again
+    assert all(b == N for ph, _, b in binned if ph != "warm") and all(b < N for ph, _, b in binned if ph == "warm")

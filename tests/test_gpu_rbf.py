@@ -219,6 +219,27 @@ def test_singular_system_raises_linalgerror(ctx):
         LocalRBFInterpolator(P, Q, neighbors=20).evaluate_grid(ax, ax, ax)
 
 
+def test_singular_count_once_after_list_overflow(ctx):
+    """Every voxel of a coplanar particle set is singular (TPS degree 1): the null-space kernel flags
+    all 32^3 voxels of the one chunk, more than its list holds, and the chunk is re-solved by the
+    pivoting kernel.  The singular voxels must be counted once (the rerun used to add its counts to
+    the first pass's), so the reported count is exactly the voxel count."""
+    import re
+
+    from ptv_interpolation_amd.rbf import LocalRBFInterpolator
+
+    rng = np.random.default_rng(15)
+    P = rng.uniform(0, 31, (4000, 3))
+    P[:, 2] = 15.5
+    Q = rng.standard_normal((len(P), 3))
+    ax = np.linspace(0, 31, 32)
+    with pytest.raises(np.linalg.LinAlgError, match="Singular matrix") as ei:
+        LocalRBFInterpolator(P, Q, neighbors=20).evaluate_grid(ax, ax, ax)
+    m = re.search(r"\((\d+) voxel system", str(ei.value))
+    print("reported:", str(ei.value)[:120], "| pivoted:", ctx.last_stats()["n_rbf_pivoted"])
+    assert m is not None and int(m.group(1)) == 32 ** 3
+
+
 def test_full_size_sampled(ctx):
     """C3 shape at a reduced grid: 128^3 over a 5M-particle-density sphere pack slice, TPS k=32,
     checked on 3000 random voxels against the oracle."""

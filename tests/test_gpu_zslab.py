@@ -86,12 +86,18 @@ def test_slab_cull_matches_whole_grid(ctx):
     assert min(binned) < len(P)
 
 
-@pytest.mark.timeout(400)
-def test_c4_rank_share_masked_with_boundary_particles(ctx):
+@pytest.mark.timeout(500)
+def test_c4_rank_share_masked_with_boundary_particles():
     """C4 (BASELINE configs[3]): 1024^3 grid / 10M sphere-pack particles + the pore-mask path
     (extract_boundary_particles, every 4th boundary voxel, zero velocity) + the fused
     main.py:195-207 epilogue; rank 2 of 8 (planes 256..383, cutting through the lower
-    spheres) on the replicated set with the slab cull; 20k sampled voxels against the oracle."""
+    spheres) on the replicated set through the shipped N > 1 path (bench.py): the per-column cull
+    map of PTV_FLAG_SLAB_CULL_AUTO on a fresh context, one cold call (every particle binned, the
+    map built) and one warm call (culled, proven on the device); both against the oracle on 20k
+    sampled voxels."""
+    import json
+    import time
+
     import torch
 
     from oracle import cpu_ref
@@ -108,22 +114,10 @@ def test_c4_rank_share_masked_with_boundary_particles(ctx):
     cols = _dev_cols(P, Q)
     ax = torch.linspace(0, G - 1, G, dtype=torch.float64, device="cuda")
     z0, z1 = zslab.rank_slab(G, world, rank)
-    out = [torch.empty((z1 - z0, G, G), dtype=torch.float64, device="cuda") for _ in range(3)]
-    state = zslab.HaloState(zslab.halo_guess(len(P), (G, G, G), 8))
-
-    def call(h):
-        return ctx.interp_knn_dev(len(P), [c.data_ptr() for c in cols], G, G, G, axes_ptrs=[ax.data_ptr()] * 3,
-                                  out_ptrs=[o.data_ptr() for o in out], k=8, mask_ptr=fluid_d.data_ptr(),
-                                  flags=_lib.FLAG_NAN_TO_NUM, z_range=(z0, z1), slab_halo=h)
-
-    zslab.interp_slab(call, state)
-    st = ctx.last_stats()
-    assert st["n_binned"] < len(P)
     rng = np.random.default_rng(4)
     sel = rng.integers(0, (z1 - z0) * G * G, 20000)
     iz, iy, ix = np.unravel_index(sel, (z1 - z0, G, G))
     q = np.stack([ix, iy, iz + z0], -1).astype(np.float64)
-    got = [o.reshape(-1)[torch.from_numpy(sel).cuda()].cpu().numpy() for o in out]
     ref = cpu_ref.interp_points(P, Q, q, "idw", 8, 2.0)
     solid = ~fluid[iz + z0, iy, ix]
     ref[solid] = 0.0
@@ -132,8 +126,31 @@ def test_c4_rank_share_masked_with_boundary_particles(ctx):
     het &= ~solid  # solid voxels are written as 0 whatever their neighbours
     print(f"C4 rank share: ties {tie.mean():.4%} of sampled voxels, value-heterogeneous (excluded) {het.mean():.4%}")
     assert het.mean() < 0.01
-    for c in range(3):
-        assert np.array_equal(got[c][~het], ref[~het, c])
+    ctx = _lib.Context(0)  # fresh: no cached cull map
+    out = [torch.empty((z1 - z0, G, G), dtype=torch.float64, device="cuda") for _ in range(3)]
+    try:
+        for call in ("cold", "warm"):
+            for o in out:
+                o.fill_(-7.0)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            ctx.interp_knn_dev(len(P), [c.data_ptr() for c in cols], G, G, G, axes_ptrs=[ax.data_ptr()] * 3,
+                               out_ptrs=[o.data_ptr() for o in out], k=8, mask_ptr=fluid_d.data_ptr(),
+                               flags=_lib.FLAG_NAN_TO_NUM | _lib.FLAG_SLAB_CULL_AUTO, z_range=(z0, z1))
+            torch.cuda.synchronize()
+            wall = (time.perf_counter() - t0) * 1e3
+            st = ctx.last_stats()
+            print("SHARE " + json.dumps({"config": "c4", "rank": rank, "world": world, "planes": [z0, z1],
+                                         "call": call, "wall_ms": round(wall, 3),
+                                         "device_ms": round(st["ms_bin"] + st["ms_cull"] + st["ms_lattice"] +
+                                                            st["ms_knn"], 3),
+                                         "n_binned": int(st["n_binned"]), "n_particles": len(P)}))
+            assert (st["n_binned"] == len(P)) if call == "cold" else (st["n_binned"] < len(P))
+            got = [o.reshape(-1)[torch.from_numpy(sel).cuda()].cpu().numpy() for o in out]
+            for c in range(3):
+                assert np.array_equal(got[c][~het], ref[~het, c])
+    finally:
+        ctx.close()
 
 
 @pytest.mark.timeout(600)

@@ -170,3 +170,45 @@ def test_launcher_slabs_and_device_list(monkeypatch):
     assert launcher.devices() == [0, 2, 3]
     monkeypatch.setenv("PTV_DEVICE", "5")
     assert launcher.devices() == [5]
+
+
+def test_launcher_recuts_slabs_from_measured_costs(monkeypatch):
+    """launcher.run_slabs re-cuts the slab bounds of later calls with the same balance key from the
+    slabs' device times (zslab.balanced_bounds), only after calls whose slabs all ran culled, at
+    most MAX_RECUTS times; a call without a key keeps even slabs.  (No GPU: contexts are stubbed.)"""
+    import numpy as np
+
+    from ptv_interpolation_amd import launcher
+
+    monkeypatch.setenv("PTV_DEVICES", "0,0,0,0")
+    monkeypatch.delenv("PTV_DEVICE", raising=False)
+    monkeypatch.setattr(launcher, "context", lambda d, slot: ("ctx", d, slot))
+    monkeypatch.setattr(launcher, "_balance", {})
+    nz = 128
+    dens = np.where(np.arange(nz) < 32, 4.0, 1.0)  # the first quarter of the planes costs 4x
+    cold = [True]
+
+    def fn(ctx, z0, z1, views):
+        for v in views:
+            v[...] = z0
+        n = 1000
+        return {"ms_bin": 0.0, "ms_cull": 0.0, "ms_lattice": 0.0, "ms_knn": float(dens[z0:z1].sum()),
+                "n_particles": n, "n_binned": n if cold[0] else n // 4}
+
+    out = [np.empty((nz, 2, 2)) for _ in range(3)]
+    even = [0, 32, 64, 96, 128]
+    launcher.run_slabs(nz, fn, out, balance_key="k")
+    assert launcher.current_bounds(nz, 4, "k") == even  # a cold call measures binning, not planes
+    cold[0] = False
+    launcher.run_slabs(nz, fn, out, balance_key="k")
+    b1 = launcher.current_bounds(nz, 4, "k")
+    assert b1 != even and b1[0] == 0 and b1[-1] == nz and b1[1] < 32
+    costs = lambda b: [dens[b[i]:b[i + 1]].sum() for i in range(4)]  # noqa: E731
+    assert max(costs(b1)) < max(costs(even))
+    launcher.run_slabs(nz, fn, out, balance_key="k")
+    b2 = launcher.current_bounds(nz, 4, "k")
+    launcher.run_slabs(nz, fn, out, balance_key="k")
+    assert launcher.current_bounds(nz, 4, "k") == b2  # MAX_RECUTS = 2 reached
+    assert launcher.current_bounds(nz, 4, "other") == even
+    # the slabs written follow the bounds in use
+    assert [out[0][z, 0, 0] for z in b2[:-1]] == b2[:-1]
