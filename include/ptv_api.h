@@ -123,7 +123,7 @@ typedef struct {
  */
 typedef struct {
     int method;          /* PTV_METHOD_* */
-    int k;               /* idw_neighbors / sibson_neighbors */
+    int k;               /* idw_neighbors / sibson_neighbors, 1 <= k <= n (k >= 128: the large-k path) */
     double power;        /* idw_power (interpolator.py:143) */
     double eps;          /* 1e-10 (interpolator.py:102, :142) */
     const uint8_t *fluid_mask;
@@ -155,7 +155,8 @@ typedef struct {
     int k;                /* rbf_neighbors, 1 <= k <= n */
     int kernel;           /* PTV_RBF_* */
     double epsilon;       /* shape parameter */
-    int degree;           /* polynomial degree, -1 = no polynomial; k + C(degree+3, 3) <= 128 */
+    int degree;           /* polynomial degree, -1 = no polynomial (systems k + C(degree+3, 3) > 128:
+                           * solved in global memory, k_rbf_huge) */
     double smoothing;     /* scalar smoothing, used when smoothing_per_point is NULL */
     const double *smoothing_per_point; /* optional (n,) array, same memory space as the particles */
     const uint8_t *fluid_mask;        /* as ptv_knn_params.fluid_mask */
@@ -240,7 +241,8 @@ typedef struct {
 
 /*
  * k-NN median/MAD outlier filter (filtering.py:5-58 remove_outliers_knn).
- * k: neighbours excluding the point itself (the reference queries k+1, :26), k <= 63;
+ * k: neighbours excluding the point itself (the reference queries k+1, :26), 1 <= k < n
+ * (k >= 127: the large-k path);
  * threshold: MAD units (:47-51); mad_eps: 1e-6 (:46).
  */
 typedef struct {

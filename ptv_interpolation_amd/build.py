@@ -23,7 +23,7 @@ BUILD = os.path.join(HERE, "csrc", "_build")
 KNN_PARTS = ["ptv_knn_k" + g + ".hip" for g in "abcdefgh"]
 SOURCES = (["ptv_api.cpp", "ptv_bin.hip", "ptv_knn.hip"] + KNN_PARTS +
            ["ptv_rbf.hip"] + ["ptv_rbf_ns_" + g + ".hip" for g in "abcd"] +
-           ["ptv_div.hip", "ptv_mask.hip", "ptv_filter.hip", "ptv_linear.hip"])
+           ["ptv_div.hip", "ptv_mask.hip", "ptv_filter.hip", "ptv_linear.hip", "ptv_knn_big.hip"])
 ARCH = os.environ.get("PTV_OFFLOAD_ARCH", "gfx950")
 # per-file extras: the local-RBF kernel keeps each voxel's system row in registers, so every
 # loop over the row must unroll fully (a partial unroll turns the row into scratch memory)

@@ -20,37 +20,13 @@
 
 #include "../../include/ptv_api.h"
 #include "ptv_kernels.hpp"
+#include "ptv_knn_big.hpp"
 
 namespace ptv {
 
 static thread_local std::string g_last_error;
 void set_error(const std::string &msg) { g_last_error = msg; }
 
-template <typename T>
-struct DevBuf {
-    T *p = nullptr;
-    size_t cap = 0;  // elements
-    int ensure(size_t n) {
-        if (n <= cap && p) return PTV_OK;
-        if (p) hipFree(p);
-        p = nullptr;
-        cap = 0;
-        size_t want = std::max<size_t>(n, 1);
-        hipError_t e = hipMalloc(&p, want * sizeof(T));
-        if (e != hipSuccess) {
-            p = nullptr;
-            set_error("hipMalloc of " + std::to_string(want * sizeof(T)) + " bytes failed: " + hipGetErrorString(e));
-            return PTV_E_NOMEM;
-        }
-        cap = want;
-        return PTV_OK;
-    }
-    void release() {
-        if (p) hipFree(p);
-        p = nullptr;
-        cap = 0;
-    }
-};
 
 }  // namespace ptv
 
@@ -65,7 +41,9 @@ struct ptv_ctx {
     hipEvent_t ev_main0 = nullptr, ev_cull0 = nullptr, ev_cull1 = nullptr;  // main-kernel start; slab cull
     bool cull_timed = false;
     bool timed_pending = false;
+    BigScratch big;  // the large-k path (ptv_knn_big.hip)
     DevBuf<double> pin[6], axes, qpts[3], out[3];
+    DevBuf<double> rbf_huge;  // k_rbf_huge's per-workgroup slices (m > 128)
     DevBuf<uint8_t> mask;
     DevBuf<uint32_t> code, perm, count, start, scanp;
     DevBuf<double4> prec, pval;
@@ -116,12 +94,6 @@ struct ptv_ctx {
     unsigned long long *h_misc = nullptr;  // pinned scratch words (cull count, halo bound, repair count)
     ptv_stats last{};
 };
-
-#define PTV_TRY(expr)               \
-    do {                            \
-        int _r = (expr);            \
-        if (_r != PTV_OK) return _r; \
-    } while (0)
 
 extern "C" {
 
@@ -232,6 +204,8 @@ int ptv_free(ptv_ctx *c) {
     for (auto &b : c->lat_recs) b.release();
     for (auto &b : c->lat_order) b.release();
     c->lat_okeys.release();
+    c->big.release();
+    c->rbf_huge.release();
     c->lat_split.release();
     for (auto &b : c->cmap) b.release();
     c->cdk.release();
@@ -383,10 +357,7 @@ int validate_knn(const ptv_particles *p, const ptv_knn_params *prm) {
         set_error("k=" + std::to_string(prm->k) + " exceeds the number of particles " + std::to_string(p->n));
         return PTV_E_ARG;
     }
-    if (kmax_for(prm->k) == 0) {
-        set_error("k=" + std::to_string(prm->k) + " exceeds the GPU k-NN list limit (127; 126 for the outlier filter)");
-        return PTV_E_UNSUPPORTED;
-    }
+    // k beyond the register lists (kmax_for(k) == 0, k >= 128) takes the large-k path (run_knn_big)
     return PTV_OK;
 }
 
@@ -925,9 +896,53 @@ int run_knn_auto(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const pt
     return PTV_E_HIP;
 }
 
+// k >= 128 (beyond the register lists): bin every particle (no lattice), then the large-k path --
+// per-query ball bound, candidate gather, segmented sort, the reference's epilogue (ptv_knn_big.hip)
+int run_knn_big(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn_params *prm, const double *ax,
+                const double *ay, const double *az, const double *qx, const double *qy, const double *qz,
+                const uint8_t *mask, double *U, double *V, double *W, hipStream_t s, ptv_stats *st) {
+    SearchParams sp = knn_search(prm);
+    sp.lattice_bounds = -1;
+    if (!(sp.cell_occupancy > 0.0)) sp.cell_occupancy = std::max(1.0, prm->k / 256.0);
+    KnnLaunch kl;
+    Binned b{};
+    c->cull_timed = false;
+    c->rbf_chunks = 0;
+    PTV_TRY(prepare(c, p, g, &sp, ax, ay, az, qx, qy, qz, s, kl, b));
+    BigQueries q;
+    q.nx = (int)g->nx;
+    q.ny = (int)g->ny;
+    q.z0 = (int)g->z_begin;
+    q.ax = ax;
+    q.ay = ay;
+    q.az = az;
+    q.px = qx;
+    q.py = qy;
+    q.pz = qz;
+    q.mask = mask;
+    BigEpilogue ep;
+    ep.method = prm->method;
+    ep.power = prm->power;
+    ep.eps = prm->eps;
+    ep.flags = prm->flags;
+    ep.U = U;
+    ep.V = V;
+    ep.W = W;
+    const int64_t nvox = (g->z_end - g->z_begin) * g->nx * g->ny;
+    PTV_TRY(run_big_knn(c->big, q, b, kl.cg, nvox, prm->k, ep, s));
+    PTV_HIP(hipEventRecord(c->ev_knn1, s));
+    c->timed_pending = true;
+    c->last.n_particles = p->n;
+    c->last.n_binned = p->n;
+    if (st) *st = c->last;
+    return PTV_OK;
+}
+
 int run_knn(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_knn_params *prm, const double *ax,
             const double *ay, const double *az, const double *qx, const double *qy, const double *qz,
             const uint8_t *mask, double *U, double *V, double *W, hipStream_t s, ptv_stats *st) {
+    if (prm->method != PTV_METHOD_IDW_RADIUS && kmax_for(prm->k) == 0)
+        return run_knn_big(c, p, g, prm, ax, ay, az, qx, qy, qz, mask, U, V, W, s, st);
     if ((prm->flags & PTV_FLAG_SLAB_CULL_AUTO) && prm->method != PTV_METHOD_IDW_RADIUS && ax != nullptr &&
         (g->z_begin > 0 || g->z_end < g->nz) && lattice_built(g, prm->lattice_bounds))
         return run_knn_auto(c, p, g, prm, ax, ay, az, mask, U, V, W, s, st);
@@ -1071,7 +1086,7 @@ int validate_rbf(const ptv_particles *p, const ptv_rbf_params *prm, int *m_out) 
         return PTV_E_ARG;
     }
     const int m = prm->k + nm;
-    if (rbf_system_size(m) == 0 || kmax_for(prm->k) == 0) {
+    if (rbf_system_size(m) == 0) {
         set_error("local RBF system of size " + std::to_string(m) + " (k=" + std::to_string(prm->k) +
                   ") exceeds the GPU limit (" + std::to_string(kRbfMaxSystem) + ")");
         return PTV_E_UNSUPPORTED;
@@ -1085,7 +1100,10 @@ int run_rbf(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_rbf
             const double *ax, const double *ay, const double *az, const double *qx, const double *qy,
             const double *qz, const double *smooth, const uint8_t *mask, double *U, double *V, double *W,
             hipStream_t s, int64_t *n_singular) {
-    const SearchParams sp{PTV_METHOD_IDW, prm->k, 2.0, 1e-10, 0u, 0.0, 0.0, 0};
+    // k >= 128: the large-k slot search (ptv_knn_big.hip; no lattice, its own cell occupancy)
+    const bool big = kmax_for(prm->k) == 0;
+    const SearchParams sp{PTV_METHOD_IDW, prm->k, 2.0, 1e-10, 0u, big ? std::max(1.0, prm->k / 256.0) : 0.0, 0.0,
+                          big ? -1 : 0};
     KnnLaunch kl;
     Binned b{};
     PTV_TRY(prepare(c, p, g, &sp, ax, ay, az, qx, qy, qz, s, kl, b));
@@ -1124,6 +1142,14 @@ int run_rbf(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_rbf
     ra.epsilon = prm->epsilon;
     ra.smoothing = prm->smoothing;
     ra.flags = prm->flags;
+    if (m > kRbfMaxSystem) {
+        // k_rbf_huge: persistent workgroups with a global-memory slice each (about 2 GB in total)
+        const size_t slice = rbf_huge_slice_doubles(m, prm->k);
+        const long long nb = std::max<long long>(64, std::min<long long>(4096, (2LL << 30) / (long long)(slice * 8)));
+        PTV_TRY(c->rbf_huge.ensure((size_t)nb * slice));
+        ra.huge_scratch = c->rbf_huge.p;
+        ra.huge_blocks = (int)nb;
+    }
     int st_out[6] = {0, 0, 0, 0, 0, 0};
     // per chunk: the voxels k_rbf_ns flagged (status[3] of its launch), whether they overflowed the
     // list (status[4]) and the running singular count (status[0]), copied on the device after each chunk
@@ -1152,7 +1178,24 @@ int run_rbf(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const ptv_rbf
         cl.mode = kModeSlots;
         cl.slots = c->slots.p;
         PTV_HIP(hipEventRecord(c->rbf_ev[3 * ch], s));
-        PTV_TRY(launch_knn(cl, b, ax, ay, az, qx, qy, qz, mask, nullptr, nullptr, nullptr, s));
+        if (big) {
+            BigQueries q;
+            q.nx = (int)g->nx;
+            q.ny = (int)g->ny;
+            q.z0 = za;
+            q.ax = ax;
+            q.ay = ay;
+            q.az = az;
+            q.px = qx;
+            q.py = qy;
+            q.pz = qz;
+            q.mask = mask;
+            BigEpilogue ep;
+            ep.slots = c->slots.p;
+            PTV_TRY(run_big_knn(c->big, q, b, kl.cg, (int64_t)(zb - za) * plane, prm->k, ep, s));
+        } else {
+            PTV_TRY(launch_knn(cl, b, ax, ay, az, qx, qy, qz, mask, nullptr, nullptr, nullptr, s));
+        }
         PTV_HIP(hipEventRecord(c->rbf_ev[3 * ch + 1], s));
         ra.z0 = za;
         ra.z1 = zb;
@@ -1923,9 +1966,9 @@ int filter_check(ptv_ctx *c, const ptv_particles *p, const ptv_filter_params *pr
         set_error("particles: n must be < 2^31");
         return PTV_E_ARG;
     }
-    if (prm->k < 1 || filter_kmax(prm->k) == 0) {
-        set_error("filter: k must be in [1, 126]");
-        return PTV_E_UNSUPPORTED;
+    if (prm->k < 1) {
+        set_error("filter: k must be >= 1");
+        return PTV_E_ARG;
     }
     if (p->n <= prm->k) {
         set_error("filter: need more particles than k (the reference skips the filter)");
@@ -1955,6 +1998,37 @@ int run_filter(ptv_ctx *c, const ptv_particles *p, const ptv_filter_params *prm,
     double r0s = kFilterR0Scale, occ = kFilterOccupancy;
     if (const char *e = dev_knob("PTV_FILTER_R0")) r0s = std::atof(e);       // dev knobs
     if (const char *e = dev_knob("PTV_FILTER_OCC")) occ = std::atof(e);
+    if (filter_kmax(prm->k) == 0) {
+        // k >= 127: the large-k path on the particles in original order (ptv_knn_big.hip)
+        const SearchParams sb{PTV_METHOD_IDW, prm->k + 1, 2.0, 1e-10, 0u, std::max(1.0, (prm->k + 1) / 256.0), 1.0, -1};
+        KnnLaunch kl;
+        Binned b{};
+        c->rbf_chunks = 0;
+        c->cull_timed = false;
+        PTV_TRY(prepare(c, p, &g, &sb, nullptr, nullptr, nullptr, g.px, g.py, g.pz, s, kl, b));
+        PTV_TRY(c->flt_spd.ensure((size_t)n));
+        PTV_TRY(launch_slot_speed(b.pval, n, c->flt_spd.p, s));
+        BigQueries q;
+        q.particles = 1;
+        q.px = p->x;
+        q.py = p->y;
+        q.pz = p->z;
+        q.pu = p->u;
+        q.pv = p->v;
+        q.pw = p->w;
+        BigEpilogue ep;
+        ep.filter = 1;
+        ep.spd = c->flt_spd.p;
+        ep.keep = keep;
+        ep.kth = kth;
+        ep.threshold = prm->threshold;
+        ep.mad_eps = prm->mad_eps;
+        PTV_TRY(run_big_knn(c->big, q, b, kl.cg, n, prm->k + 1, ep, s));
+        PTV_HIP(hipEventRecord(c->ev_knn1, s));
+        c->timed_pending = true;
+        c->last.n_voxels = n;
+        return PTV_OK;
+    }
     const SearchParams sp{PTV_METHOD_IDW, prm->k + 1, 2.0, 1e-10, 0u, occ, r0s, -1};
     KnnLaunch kl;
     Binned b{};

@@ -36,6 +36,12 @@ void set_error(const std::string &msg);
         }                                                                          \
     } while (0)
 
+#define PTV_TRY(expr)               \
+    do {                            \
+        int _r = (expr);            \
+        if (_r != PTV_OK) return _r; \
+    } while (0)
+
 // ---------------------------------------------------------------------------
 // Binning cell grid: a uniform grid of cells over the particle/query bounding
 // box in linear (z, y, x) order, x fastest.  After the counting sort, every

@@ -208,7 +208,7 @@ int launch_linear_brute(const LinearKernelArgs &a, int nflag, const double *ax, 
 
 // ---- local RBF (ptv_rbf.hip) ----
 constexpr int kRbfNsCap = 1 << 14;   // voxels per launch k_rbf_ns may hand to the pivoting kernel
-constexpr int kRbfMaxSystem = 128;  // k + #monomials per voxel system (> 64: k_rbf_big, LDS-resident)
+constexpr int kRbfMaxSystem = 128;  // k + #monomials per voxel system in LDS (> 64: k_rbf_big; larger: k_rbf_huge, global)
 
 struct RbfKernelArgs {
     int nx, ny;      // grid plane
@@ -230,7 +230,12 @@ struct RbfKernelArgs {
     const int *vcount;
     unsigned long long *stamps;  // dev builds (PTV_NS_STAMP): per-wave phase cycles of k_rbf_ns, 8 per wave
     long long stamp_cap;
+    // m > kRbfMaxSystem (k_rbf_huge): huge_blocks persistent workgroups, each with a slice of
+    // rbf_huge_slice_doubles(m, k) doubles of huge_scratch
+    double *huge_scratch;
+    int huge_blocks;
 };
+size_t rbf_huge_slice_doubles(int m, int k);
 
 // null-space local-RBF kernels k_rbf_ns<NC, NP> (ptv_rbf_ns.hpp), one translation unit per
 // row-slot count NC (16, 20, 24, 32); np = number of monomials (1, 4 or 10)

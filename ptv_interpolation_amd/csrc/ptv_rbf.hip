@@ -545,6 +545,231 @@ __global__ __launch_bounds__(64) void k_rbf_big(RbfKernelArgs a, const double4 *
 }
 
 // ---------------------------------------------------------------------------
+// Systems of m > 128 (k >= 125 with a linear polynomial, any k >= 129): k_rbf_big's algorithm --
+// the same entries, idamax pivots with explicit row swaps, dgetf2's reciprocal multipliers, fma
+// updates, the reciprocal back substitution -- with the augmented matrix and the neighbour tables
+// in a global-memory slice per workgroup of a persistent grid (they outgrow the LDS).  The LU
+// streams its trailing matrix through L2 / HBM each column: correctness over speed, for a
+// configuration the reference's RBFInterpolator(neighbors=k) also takes (interpolator.py:157-195).
+// ---------------------------------------------------------------------------
+// order this wave's global stores before its later loads (one wave per workgroup)
+__device__ __forceinline__ void huge_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+size_t rbf_huge_slice_doubles(int m, int k) {
+    // A (m x (m + 3)); ye, yh, rec, val (k double4 each); sv (m double4); sid (k u32)
+    return (size_t)m * (m + 3) + 4 * (4 * (size_t)k + (size_t)m) + ((size_t)k + 1) / 2 + 8;
+}
+
+__global__ __launch_bounds__(64) void k_rbf_huge(RbfKernelArgs a, const double4 *__restrict__ prec,
+                                                 const double4 *__restrict__ pval, const uint32_t *__restrict__ slots,
+                                                 const double *__restrict__ ax, const double *__restrict__ ay,
+                                                 const double *__restrict__ az, const double *__restrict__ qpx,
+                                                 const double *__restrict__ qpy, const double *__restrict__ qpz,
+                                                 const double *__restrict__ smooth, const int *__restrict__ pw,
+                                                 const uint8_t *__restrict__ mask, double *__restrict__ U,
+                                                 double *__restrict__ V, double *__restrict__ W,
+                                                 int *__restrict__ status, double *__restrict__ scratch, size_t slice,
+                                                 long long nvox) {
+    const int lane = threadIdx.x;
+    const int k = a.k, m = a.m, ld = m + 3;
+    double *A = scratch + (size_t)blockIdx.x * slice;                // row i at A + i * ld
+    double4 *ye = reinterpret_cast<double4 *>(A + (size_t)m * ld);   // eps-scaled (x, y, z, id), id order
+    double4 *yh = ye + k;                                            // yhat, id order
+    double4 *rec = yh + k;                                           // records, list order
+    double4 *val = rec + k;                                          // values, list order
+    double4 *sv = val + k;                                           // values (id order), later the solution
+    uint32_t *sid = reinterpret_cast<uint32_t *>(sv + m);            // ids, list order
+    const long long plane = (long long)a.nx * a.ny;
+    const double eps = a.epsilon;
+    for (long long v = blockIdx.x; v < nvox; v += gridDim.x) {
+        const int iz = a.z0 + (int)(v / plane);
+        const long long rem = v % plane;
+        const int iy = (int)(rem / a.nx), ix = (int)(rem % a.nx);
+        const size_t vfull = (size_t)iz * plane + rem;
+        const size_t vo = (size_t)(iz - a.out_z0) * plane + rem;
+        if (mask != nullptr && mask[vfull] == 0) {  // wave-uniform (one voxel per wave)
+            if (lane == 0) {
+                U[vo] = 0.0;
+                V[vo] = 0.0;
+                W[vo] = 0.0;
+            }
+            continue;
+        }
+        // ---- 1. the k neighbours, ranked by particle index ----
+        double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int j = lane; j < k; j += 64) {
+            const uint32_t s = slots[(size_t)v * k + j];
+            const double4 r = prec[s];
+            rec[j] = r;
+            val[j] = pval[s];
+            sid[j] = (uint32_t)r.w;
+            mn[0] = fmin(mn[0], r.x);
+            mn[1] = fmin(mn[1], r.y);
+            mn[2] = fmin(mn[2], r.z);
+            mx[0] = fmax(mx[0], r.x);
+            mx[1] = fmax(mx[1], r.y);
+            mx[2] = fmax(mx[2], r.z);
+        }
+        double sh[3], scl[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const double lo = seg_min<64>(mn[c]), hi = seg_max<64>(mx[c]);
+            sh[c] = (hi + lo) / 2.0;  // _build_system: shift = (max + min)/2, scale = (max - min)/2 (0 -> 1)
+            scl[c] = (hi - lo) / 2.0;
+            if (scl[c] == 0.0) scl[c] = 1.0;
+        }
+        huge_sync();
+        for (int j = lane; j < k; j += 64) {
+            const uint32_t idj = sid[j];
+            int rank = 0;
+            for (int t = 0; t < k; ++t) {
+                const uint32_t o = sid[t];
+                rank += (o < idj || (o == idj && t < j)) ? 1 : 0;
+            }
+            const double4 r = rec[j];
+            ye[rank] = make_double4(r.x * eps, r.y * eps, r.z * eps, (double)idj);
+            yh[rank] = make_double4((r.x - sh[0]) / scl[0], (r.y - sh[1]) / scl[1], (r.z - sh[2]) / scl[2], 0.0);
+            sv[rank] = val[j];
+        }
+        huge_sync();
+        // ---- 2. the augmented system, row by row ----
+        for (int i = 0; i < m; ++i) {
+            const bool krow = i < k;
+            const double4 yi = krow ? ye[i] : make_double4(0.0, 0.0, 0.0, 0.0);
+            const double4 hi = krow ? yh[i] : make_double4(0.0, 0.0, 0.0, 0.0);
+            const int tcode = krow ? 0 : pw[i - k];
+            double si = 0.0;
+            if (krow) si = smooth != nullptr ? smooth[(size_t)yi.w] : a.smoothing;
+            for (int j = lane; j < ld; j += 64) {
+                double e = 0.0;
+                if (j < m) {
+                    if (krow) {
+                        if (j < k) {
+                            const double4 yj = ye[j];
+                            const double dx = yi.x - yj.x, dy = yi.y - yj.y, dz = yi.z - yj.z;
+                            e = rbf_phi_rt(a.kernel, sqrt((dx * dx + dy * dy) + dz * dz));
+                            if (j == i) e = e + si;
+                        } else {
+                            e = mono(hi.x, hi.y, hi.z, pw[j - k]);
+                        }
+                    } else if (j < k) {
+                        const double4 hj = yh[j];
+                        e = mono(hj.x, hj.y, hj.z, tcode);
+                    }
+                } else if (krow) {
+                    const double4 dv = sv[i];
+                    e = j == m ? dv.x : (j == m + 1 ? dv.y : dv.z);
+                }
+                A[(size_t)i * ld + j] = e;
+            }
+        }
+        huge_sync();
+        // ---- 3. LU with partial pivoting (explicit row swaps), the right-hand sides along ----
+        bool singular = false;
+        for (int c = 0; c < m; ++c) {
+            double best = -1.0;
+            int brow = m;
+            for (int i = c + lane; i < m; i += 64) {
+                const double q = fabs(A[(size_t)i * ld + c]);
+                if (q > best) {  // rows ascend per lane: the first maximum is the lowest row
+                    best = q;
+                    brow = i;
+                }
+            }
+            const double bmax = seg_max<64>(best);
+            const int p = -(int)seg_max<64>(best == bmax ? -(double)brow : -(double)m);  // lowest row holding it
+            singular = singular || !(bmax > 0.0);
+            if (p != c) {
+                for (int j = lane; j < ld; j += 64) {
+                    const double t = A[(size_t)c * ld + j];
+                    A[(size_t)c * ld + j] = A[(size_t)p * ld + j];
+                    A[(size_t)p * ld + j] = t;
+                }
+            }
+            huge_sync();
+            const double piv = A[(size_t)c * ld + c];
+            for (int i = c + 1 + lane; i < m; i += 64) {
+                const double aic = A[(size_t)i * ld + c];
+                A[(size_t)i * ld + c] = piv != 0.0 ? elim_multiplier(aic, piv) : 0.0;
+            }
+            huge_sync();
+            for (int j = c + 1 + lane; j < ld; j += 64) {
+                const double pj = A[(size_t)c * ld + j];
+                for (int i = c + 1; i < m; ++i) {
+                    const double l = A[(size_t)i * ld + c];
+                    A[(size_t)i * ld + j] = fma(-l, pj, A[(size_t)i * ld + j]);
+                }
+            }
+            huge_sync();
+        }
+        // ---- 4. back substitution (column oriented), x_c = b_c * (1 / u_cc) into sv ----
+        for (int c = m - 1; c >= 0; --c) {
+            if (lane == 0) {
+                const double rd = 1.0 / A[(size_t)c * ld + c];
+                sv[c] = make_double4(A[(size_t)c * ld + m] * rd, A[(size_t)c * ld + m + 1] * rd,
+                                     A[(size_t)c * ld + m + 2] * rd, 0.0);
+            }
+            huge_sync();
+            const double4 xc = sv[c];
+            for (int i = lane; i < c; i += 64) {
+                const double u = A[(size_t)i * ld + c];
+                A[(size_t)i * ld + m] = fma(-u, xc.x, A[(size_t)i * ld + m]);
+                A[(size_t)i * ld + m + 1] = fma(-u, xc.y, A[(size_t)i * ld + m + 1]);
+                A[(size_t)i * ld + m + 2] = fma(-u, xc.z, A[(size_t)i * ld + m + 2]);
+            }
+            huge_sync();
+        }
+        // ---- 5. evaluate at the voxel ----
+        double qx, qy, qz;
+        if (a.separable) {
+            qx = ax[ix];
+            qy = ay[iy];
+            qz = az[iz];
+        } else {
+            qx = qpx[vfull];
+            qy = qpy[vfull];
+            qz = qpz[vfull];
+        }
+        double o[3] = {0.0, 0.0, 0.0};
+        for (int j = lane; j < m; j += 64) {
+            double e;
+            if (j < k) {
+                const double4 yj = ye[j];
+                const double dx = qx * eps - yj.x, dy = qy * eps - yj.y, dz = qz * eps - yj.z;
+                e = rbf_phi_rt(a.kernel, sqrt((dx * dx + dy * dy) + dz * dz));
+            } else {
+                e = mono((qx - sh[0]) / scl[0], (qy - sh[1]) / scl[1], (qz - sh[2]) / scl[2], pw[j - k]);
+            }
+            const double4 cf = sv[j];
+            o[0] += e * cf.x;
+            o[1] += e * cf.y;
+            o[2] += e * cf.z;
+        }
+        double o0 = seg_sum<64>(o[0]), o1 = seg_sum<64>(o[1]), o2 = seg_sum<64>(o[2]);
+        if (lane == 0) {
+            if (singular) {
+                atomicAdd(&status[0], 1);
+                atomicMin(&status[1], (int)min((long long)vfull, 0x7fffffffLL));
+            }
+            if (a.flags & PTV_FLAG_NAN_TO_NUM) {
+                auto fix = [](double x) { return x != x ? 0.0 : (x == INFINITY ? DBL_MAX : (x == -INFINITY ? -DBL_MAX : x)); };
+                o0 = fix(o0);
+                o1 = fix(o1);
+                o2 = fix(o2);
+            }
+            U[vo] = o0;
+            V[vo] = o1;
+            W[vo] = o2;
+        }
+        huge_sync();  // the slice is rewritten by the next voxel
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Symmetric positive definite systems: kernel gaussian / inverse_multiquadric /
 // inverse_quadratic with degree -1 (no polynomial block, m = k) and smoothing >= 0.  The
 // matrix [phi(eps |y_i - y_j|) + s delta_ij] is SPD for distinct points, so Gaussian
@@ -1161,8 +1386,8 @@ static bool rbf_ns(const RbfKernelArgs &ka, const double *smooth, long long nvox
 }
 
 int rbf_system_size(int m) {
-    if (m < 1 || m > kRbfMaxSystem) return 0;
-    return m <= 64 ? (m + 7) & ~7 : m;  // k_rbf_local pads to a multiple of 8; k_rbf_big takes m
+    if (m < 1) return 0;
+    return m <= 64 ? (m + 7) & ~7 : m;  // k_rbf_local pads to a multiple of 8; k_rbf_big / k_rbf_huge take m
 }
 
 template <int M>
@@ -1193,6 +1418,20 @@ int launch_rbf(const RbfKernelArgs &ka, const Binned &b, const uint32_t *slots, 
     if ((nvox + 3) / 4 > 0x7fffffffLL) {
         set_error("grid chunk too large for one launch");
         return PTV_E_ARG;
+    }
+    if (M > kRbfMaxSystem) {
+        // persistent 64-lane workgroups, each with its global-memory slice (ka.huge_scratch, sized by
+        // the host: ka.huge_blocks slices of rbf_huge_slice_doubles(m, k))
+        if (ka.huge_scratch == nullptr || ka.huge_blocks <= 0) {
+            set_error("local RBF: the m > 128 kernel needs its scratch");
+            return PTV_E_ARG;
+        }
+        const long long blocks = std::min<long long>(ka.huge_blocks, nvox);
+        hipLaunchKernelGGL(k_rbf_huge, dim3((unsigned)blocks), dim3(64), 0, s, ka, b.prec, b.pval, slots, ax, ay, az,
+                           qx, qy, qz, smooth, pw, mask, U, V, W, status, ka.huge_scratch,
+                           rbf_huge_slice_doubles(ka.m, ka.k), nvox);
+        PTV_HIP(hipGetLastError());
+        return PTV_OK;
     }
     if (M > 64) {
         // one 64-lane block per voxel: sub-launches of whole planes, at most 2^26 voxels (2^32 work

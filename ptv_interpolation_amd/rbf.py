@@ -31,7 +31,7 @@ AVAILABLE = {"linear", "thin_plate_spline", "cubic", "quintic", "multiquadric", 
              "inverse_quadratic", "gaussian"}
 SCALE_INVARIANT = {"linear", "thin_plate_spline", "cubic", "quintic"}
 NAME_TO_MIN_DEGREE = {"multiquadric": 0, "linear": 0, "thin_plate_spline": 1, "cubic": 1, "quintic": 2}
-MAX_SYSTEM = 128  # include/ptv_api.h: k + C(degree + 3, 3) <= 128
+MAX_SYSTEM = 128  # systems up to this size are solved in LDS; larger ones in global memory (k_rbf_huge)
 
 
 def _device():
@@ -103,9 +103,6 @@ class LocalRBFInterpolator:
         if neighbors is None:
             raise NotImplementedError("RBFInterpolator(neighbors=None) builds one global system; only the local "
                                       "(neighbors=k) form used by interpolate_field runs on the GPU")
-        if neighbors + nmonos > MAX_SYSTEM:
-            raise NotImplementedError(f"local system of size {neighbors + nmonos} exceeds the GPU limit "
-                                      f"({MAX_SYSTEM})")
         self.y, self.d = y, d
         self.neighbors = neighbors
         self.smoothing = smoothing

@@ -61,8 +61,9 @@ def test_k_above_n_raises(ctx):
     P, Q, ax = _random_case(3, 100, 6)
     with pytest.raises(ValueError):
         ctx.interp_knn(P, Q, axes=(ax, ax, ax), k=101)
-    with pytest.raises(NotImplementedError):
-        ctx.interp_knn(np.tile(P, (2, 1)), np.tile(Q, (2, 1)), axes=(ax, ax, ax), k=128)
+    # k >= 128 is served by the large-k path (tests/test_gpu_bigk.py), k > n still raises there
+    with pytest.raises(ValueError):
+        ctx.interp_knn(P, Q, axes=(ax, ax, ax), k=200)
 
 
 @pytest.mark.parametrize("k", [14, 20, 50])

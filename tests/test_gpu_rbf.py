@@ -148,8 +148,29 @@ def test_large_systems_vs_oracle(ctx, kernel, k, degree, eps):
         err = normwise(a, b)
         print(f"{kernel} k={k}: normwise {err:.2e}")
         assert err <= TOL
-    with pytest.raises(NotImplementedError):
-        LocalRBFInterpolator(P, Q, neighbors=126, kernel="quintic")  # m = 136 > 128
+
+
+@pytest.mark.parametrize("kernel,k,degree,eps", [
+    ("thin_plate_spline", 126, None, None),  # m = 130: past the LDS kernel
+    ("quintic", 126, None, None),            # m = 136
+    ("linear", 150, None, None),             # m = 154, k >= 128: the large-k slot search too
+    ("inverse_multiquadric", 200, -1, 0.8),  # m = 200
+])
+def test_huge_systems_vs_oracle(ctx, kernel, k, degree, eps):
+    """Systems of m > 128 (k_rbf_huge: the system in a global-memory slice per workgroup) and
+    neighbour counts k >= 128 (the large-k slot search, ptv_knn_big.hip) against the oracle:
+    RBFInterpolator(neighbors=k) takes any k (interpolator.py:162-167)."""
+    from oracle import cpu_ref
+    from ptv_interpolation_amd.rbf import LocalRBFInterpolator
+
+    P, Q, ax = _rand_case(k * 13 + len(kernel), 4000, 6)
+    it = LocalRBFInterpolator(P, Q, neighbors=k, kernel=kernel, epsilon=eps, degree=degree)
+    U, V, W = it.evaluate_grid(ax, ax, ax)
+    ref = cpu_ref.rbf_local_grid(P, Q, ax, ax, ax, k, kernel, eps, degree)
+    for a, b in zip((U, V, W), ref):
+        err = normwise(a, b)
+        print(f"{kernel} k={k}: normwise {err:.2e}")
+        assert err <= TOL
 
 
 def test_smoothing_scalar_and_per_point(ctx):
