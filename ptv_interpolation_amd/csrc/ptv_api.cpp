@@ -525,7 +525,13 @@ int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchP
     int nlat = 0;
     if (sep && prm->lattice_bounds >= 0) {
         int n[3] = {(int)g->nx, (int)g->ny, (int)(z1 - z0)};
-        const double *src[3] = {ax, ay, az + z0};
+        // every level's axes from the grid's in one launch (each level takes every 4th point of the
+        // one above it, plus the last)
+        SubsampleBatch sb{};
+        for (int d = 0; d < 3; ++d) sb.n0[d] = n[d];
+        sb.base[0] = ax;
+        sb.base[1] = ay;
+        sb.base[2] = az + z0;
         while (nlat < kMaxLattice) {
             const long long pts = (long long)n[0] * n[1] * n[2];
             long long stop = kLatticeStopPoints;
@@ -544,13 +550,15 @@ int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchP
             L.dk = c->lat_dk[nlat].p;
             L.recs = nullptr;
             double *dst[3] = {L.ax, L.ay, L.az};
-            for (int d = 0; d < 3; ++d) PTV_TRY(launch_subsample(src[d], n[d], kLatticeStep, dst[d], L.n[d], s));
             for (int d = 0; d < 3; ++d) {
-                src[d] = dst[d];
+                sb.n[nlat][d] = L.n[d];
+                sb.out[nlat][d] = dst[d];
                 n[d] = L.n[d];
             }
             ++nlat;
         }
+        sb.nlev = nlat;
+        if (nlat > 0) PTV_TRY(launch_subsample_levels(sb, kLatticeStep, s));
     }
 
     // 4. launch template (k-NN search + consumer)
@@ -726,19 +734,17 @@ int run_knn_auto(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const pt
     const SearchParams sp = knn_search(prm);
     const int64_t n = p->n;
     const double *src[6] = {p->x, p->y, p->z, p->u, p->v, p->w};
-    PTV_TRY(c->cfp.ensure(6 * kFingerprint));
-    PTV_TRY(launch_fingerprint(src, n, c->cfp.p, s));
-    std::vector<double> &key = c->ckey_new;
     // the fingerprint, then the grid's axis values: the map and the cached lattice bounds belong to
     // lattice positions, and a reused axis buffer (the host path's c->axes, a recycled torch
-    // allocation) can hold other coordinates under the same pointer
-    const size_t nfp = 6 * kFingerprint;
-    key.assign(nfp + (size_t)(g->nx + g->ny + g->nz), 0.0);
-    PTV_HIP(hipMemcpyAsync(key.data(), c->cfp.p, nfp * sizeof(double), hipMemcpyDeviceToHost, s));
-    PTV_HIP(hipMemcpyAsync(key.data() + nfp, ax, (size_t)g->nx * sizeof(double), hipMemcpyDefault, s));
-    PTV_HIP(hipMemcpyAsync(key.data() + nfp + g->nx, ay, (size_t)g->ny * sizeof(double), hipMemcpyDefault, s));
-    PTV_HIP(hipMemcpyAsync(key.data() + nfp + g->nx + g->ny, az, (size_t)g->nz * sizeof(double), hipMemcpyDefault,
-                           s));
+    // allocation) can hold other coordinates under the same pointer.  Gathered on the device and
+    // read back in one copy (one copy per array cost ~20 us each)
+    const size_t nfp = 6 * kFingerprint, nkey = nfp + (size_t)(g->nx + g->ny + g->nz);
+    PTV_TRY(c->cfp.ensure(nkey));
+    PTV_TRY(launch_fingerprint(src, n, c->cfp.p, s));
+    PTV_TRY(launch_concat3(ax, (int)g->nx, ay, (int)g->ny, az, (int)g->nz, c->cfp.p + nfp, s));
+    std::vector<double> &key = c->ckey_new;
+    key.assign(nkey, 0.0);
+    PTV_HIP(hipMemcpyAsync(key.data(), c->cfp.p, nkey * sizeof(double), hipMemcpyDeviceToHost, s));
     PTV_HIP(hipStreamSynchronize(s));
     for (const void *q : {(const void *)p->x, (const void *)p->y, (const void *)p->z, (const void *)p->u,
                           (const void *)p->v, (const void *)p->w, (const void *)ax, (const void *)ay,

@@ -143,6 +143,20 @@ int launch_count_bound(const CellGrid &g, const uint32_t *cstart, const double *
 
 // out[j] = in[min(step*j, n-1)] for j < nout (lattice axes)
 int launch_subsample(const double *in, int n, int step, double *out, int nout, hipStream_t s);
+// every lattice level's axes in one launch: level l axis d has n[l][d] points, level l's point j is
+// level (l - 1)'s point min(step j, n[l-1][d] - 1), level -1 = base[d] with n0[d] points
+constexpr int kMaxSubsampleLevels = 8;
+struct SubsampleBatch {
+    const double *base[3];
+    int n0[3];
+    int nlev;
+    int n[kMaxSubsampleLevels][3];
+    double *out[kMaxSubsampleLevels][3];
+};
+int launch_subsample_levels(const SubsampleBatch &b, int step, hipStream_t s);
+// out = a[0..na) ++ b[0..nb) ++ c[0..nc) (device arrays)
+int launch_concat3(const double *a, int na, const double *b, int nb, const double *c, int nc, double *out,
+                   hipStream_t s);
 
 // Smallest z halo that makes a slab-culled k-NN exact, from the finest lattice's k-th
 // distance bounds dk over (nx, ny, nz) lattice points with axes lax, lay, laz and the slab's

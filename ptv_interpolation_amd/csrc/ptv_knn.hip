@@ -93,6 +93,46 @@ __global__ void k_subsample(const double *__restrict__ in, int n, int step, doub
     if (j < nout) out[j] = in[min(j * step, n - 1)];
 }
 
+__global__ void k_subsample_levels(SubsampleBatch b, int step) {
+    const int l = blockIdx.y / 3, d = blockIdx.y % 3;
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= b.n[l][d]) return;
+    long long idx = j;
+    for (int lev = l; lev >= 0; --lev) idx = min(idx * step, (long long)(lev == 0 ? b.n0[d] : b.n[lev - 1][d]) - 1);
+    b.out[l][d][j] = b.base[d][idx];
+}
+
+int launch_subsample_levels(const SubsampleBatch &b, int step, hipStream_t s) {
+    if (b.nlev <= 0) return PTV_OK;
+    if (b.nlev > kMaxSubsampleLevels) {
+        set_error("lattice: too many levels");
+        return PTV_E_ARG;
+    }
+    int mx = 1;
+    for (int l = 0; l < b.nlev; ++l)
+        for (int d = 0; d < 3; ++d) mx = std::max(mx, b.n[l][d]);
+    hipLaunchKernelGGL(k_subsample_levels, dim3((mx + 255) / 256, 3 * b.nlev), dim3(256), 0, s, b, step);
+    PTV_HIP(hipGetLastError());
+    return PTV_OK;
+}
+
+__global__ void k_concat3(const double *__restrict__ a, int na, const double *__restrict__ b, int nb,
+                          const double *__restrict__ c, int nc, double *__restrict__ out) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < na) out[j] = a[j];
+    else if (j < na + nb) out[j] = b[j - na];
+    else if (j < na + nb + nc) out[j] = c[j - na - nb];
+}
+
+int launch_concat3(const double *a, int na, const double *b, int nb, const double *c, int nc, double *out,
+                   hipStream_t s) {
+    const int n = na + nb + nc;
+    if (n <= 0) return PTV_OK;
+    hipLaunchKernelGGL(k_concat3, dim3((n + 255) / 256), dim3(256), 0, s, a, na, b, nb, c, nc, out);
+    PTV_HIP(hipGetLastError());
+    return PTV_OK;
+}
+
 int launch_subsample(const double *in, int n, int step, double *out, int nout, hipStream_t s) {
     hipLaunchKernelGGL(k_subsample, dim3((nout + 255) / 256), dim3(256), 0, s, in, n, step, out, nout);
     PTV_HIP(hipGetLastError());
@@ -388,6 +428,8 @@ int launch_knn(const KnnLaunch &a, const Binned &b, const double *ax, const doub
     ka.split = 0;
     ka.split_tiles = 0;
     ka.split_out = nullptr;
+    ka.split_lb = 0;
+    ka.order_skip = 0;
     if (a.mode == kModeKDist && a.split > 1 && a.split_blocks > 0 && a.order != nullptr && a.split_out != nullptr) {
         // lattice level: the first split_blocks blocks of the longest-first order (the void tiles)
         // with `split` waves per tile, the rest of the order as usual, then the merge of the split
@@ -399,20 +441,18 @@ int launch_knn(const KnnLaunch &a, const Binned &b, const double *ax, const doub
         ks.split_out = a.split_out;
         PTV_HIP(hipMemsetAsync(a.split_out, 0xff, kdist_split_slots(a.split, nsb, km) * sizeof(uint32_t), s));
         const long long sblocks = ((long long)ks.split_tiles * a.split + 3) / 4;
-        if (sblocks > 0x7fffffffLL) {
+        // one launch: the split waves first (the void tiles lead the longest-first order), then
+        // the rest of the order as ordinary blocks (two launches serialised the split part)
+        const long long total = sblocks + (nblocks - nsb);
+        if (total > 0x7fffffffLL) {
             set_error("split lattice launch too large");
             return PTV_E_ARG;
         }
-        ks.nblocks = (int)sblocks;
-        int rc = launch_kmax(km, false, grid_for(sblocks), s, ks, b, ax, ay, az, qx, qy, qz, mask, U, V, W);
+        ks.nblocks = (int)total;
+        ks.split_lb = (int)sblocks;
+        ks.order_skip = (int)(nsb - sblocks);
+        int rc = launch_kmax(km, false, grid_for(total), s, ks, b, ax, ay, az, qx, qy, qz, mask, U, V, W);
         if (rc != PTV_OK) return rc;
-        if (nblocks > nsb) {
-            KnnKernelArgs kn = ka;
-            kn.order = a.order + nsb;
-            kn.nblocks = (int)(nblocks - nsb);
-            rc = launch_kmax(km, false, grid_for(kn.nblocks), s, kn, b, ax, ay, az, qx, qy, qz, mask, U, V, W);
-            if (rc != PTV_OK) return rc;
-        }
         ks.mode = kModeKDistMerge;
         return launch_kmax(km, false, grid_for(nsb), s, ks, b, ax, ay, az, qx, qy, qz, mask, U, V, W);
     }

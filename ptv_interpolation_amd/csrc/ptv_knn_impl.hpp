@@ -167,6 +167,10 @@ struct KnnKernelArgs {
     int split;
     int split_tiles;
     uint32_t *split_out;
+    // a fused lattice launch: its first split_lb blocks are the split waves, the others ordinary
+    // blocks of the order from entry lb + order_skip (0 and 0: every block one kind)
+    int split_lb;
+    int order_skip;
 };
 
 // Packed keys (the KMAX >= 16 lists).  A key is the candidate's exact f64 d2 with the low B
@@ -826,7 +830,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
     // split lattice launch: this wave's part of its tile's cell rows (wave-uniform)
     int part = 0, nparts = 1;
     bool split_epi = false;
-    if (MODE == kModeKDist && a.split > 0) {
+    if (MODE == kModeKDist && a.split > 0 && lb < a.split_lb) {
         const int e = lb * 4 + wid;
         const int t = e / a.split;
         if (t >= a.split_tiles) return;
@@ -843,7 +847,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
         b = (int)(t >> 2);
         tw = (int)(t & 3u);
     } else {
-        b = a.order != nullptr ? a.order[lb] : xcd_block(lb, a.nblocks);
+        b = a.order != nullptr ? a.order[lb + a.order_skip] : xcd_block(lb, a.nblocks);
         tw = wid;
     }
     b = __builtin_amdgcn_readfirstlane(b);  // wave-uniform (the tile list is read per wave)

@@ -167,10 +167,18 @@ def test_huge_systems_vs_oracle(ctx, kernel, k, degree, eps):
     it = LocalRBFInterpolator(P, Q, neighbors=k, kernel=kernel, epsilon=eps, degree=degree)
     U, V, W = it.evaluate_grid(ax, ax, ax)
     ref = cpu_ref.rbf_local_grid(P, Q, ax, ax, ax, k, kernel, eps, degree)
-    for a, b in zip((U, V, W), ref):
-        err = normwise(a, b)
-        print(f"{kernel} k={k}: normwise {err:.2e}")
-        assert err <= TOL
+    # the larger systems are worse conditioned: the bar is the exact answer of the same systems
+    # (extended precision), gpu-vs-exact <= max(1e-10, TRUTH_FACTOR x lapack-vs-exact), as for C3
+    Z, Y, X = np.meshgrid(ax, ax, ax, indexing="ij")
+    q = np.stack([X.ravel(), Y.ravel(), Z.ravel()], -1)
+    ext = cpu_ref.rbf_local_points(P, Q, q, k, kernel, eps, degree, solver="extended")
+    for c, (a, b) in enumerate(zip((U, V, W), ref)):
+        e_ref = normwise(a, b)
+        e_exact = normwise(a.ravel(), ext[:, c])
+        gap = normwise(b.ravel(), ext[:, c])
+        print(f"{kernel} k={k} m={k + it.nmonos}: gpu-vs-lapack {e_ref:.2e}, "
+              f"gpu-vs-exact {e_exact:.2e}, lapack-vs-exact {gap:.2e}")
+        assert e_exact <= max(TOL, TRUTH_FACTOR * gap)
 
 
 def test_smoothing_scalar_and_per_point(ctx):
