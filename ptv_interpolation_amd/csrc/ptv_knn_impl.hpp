@@ -81,6 +81,9 @@ namespace ptv {
 // between passes; longer ones re-gather the records every pass (Sibson: four passes)
 #define PTV_KNN_KEEP_MAX 56
 #endif
+#ifndef PTV_FILTER_SEEDED
+#define PTV_FILTER_SEEDED 0  // dev builds: 1 = the filter's first gather pass at its wave's largest seed bound
+#endif
 #ifndef PTV_STAMP_SEEDSPLIT
 #define PTV_STAMP_SEEDSPLIT 0  // dev stamp builds: union-seed counting passes stamped as 'setup'
 #endif
@@ -1223,42 +1226,89 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
             }
         }
         if constexpr (MODE == kModeFilter) {
-            // ---- seeds (outlier filter, filtering.py:26): the tile's queries are 64 distinct
-            //      particles of one Morton blob, so every lane's k-th (= k + 1 of the filter)
-            //      smallest distance to the tile's real queries bounds its own k-th neighbour
-            //      distance; the padding queries (q_orig ~0, repeats of the last particle) are
-            //      left out. ----
-            const bool realq = active && a.fe.q_orig[vfull] != 0xffffffffu;
-            const unsigned long long rm = __builtin_amdgcn_ballot_w64(realq);
-            const int nu = __builtin_popcountll(rm);
-            if (realq) {
-                const int pos = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(rm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)rm, 0u));
-                fbx[pos] = qfx;
-                fby[pos] = qfy;
-                fbz[pos] = qfz;
+            // ---- seeds (outlier filter, filtering.py:26): the tile's queries are the 64 distinct
+            //      particles of one Morton blob; with the blobs before and after it (the tiles g - 1
+            //      and g + 1 of the query layout, ptv_filter.hip pos_of) every lane's k-th (= k + 1
+            //      of the filter) smallest distance to those <= 192 particles bounds its own k-th
+            //      neighbour distance.  A blob's edge lanes see few of their neighbours in the blob
+            //      alone: measured offline on the sphere pack (1M particles, k + 1 = 26) the bound is
+            //      1.66x the true distance on average with the blob, 1.22x with its two neighbours,
+            //      and the worst lane of a wave (which sets the wave's insertion rounds) 6x (volume)
+            //      instead of 237x.  The padding queries (q_orig ~0) are left out. ----
+            const long long ntile = ((long long)a.nx * a.ny * a.nz) >> 6;
+            const long long g = (long long)tz * a.ntx + tx;  // this tile = Morton blob g
+            auto qpos = [&](long long gt) -> size_t {
+                const long long gz = gt / a.ntx, gx = gt - gz * a.ntx;
+                return ((size_t)(gz * 4 + (lane >> 4)) * a.ny + ((lane >> 2) & 3)) * a.nx + gx * 4 + (lane & 3);
+            };
+            float nx_[2], ny_[2], nz_[2];
+            bool nreal[2];
+            double pmn = 0.0;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const long long gn = g + (h ? 1 : -1);
+                nreal[h] = false;
+                nx_[h] = ny_[h] = nz_[h] = 0.f;
+                if (gn >= 0 && gn < ntile) {
+                    const size_t pn = qpos(gn);
+                    if (a.fe.q_orig[pn] != 0xffffffffu) {
+                        nreal[h] = true;
+                        nx_[h] = (float)(qpx[pn] - tcx);
+                        ny_[h] = (float)(qpy[pn] - tcy);
+                        nz_[h] = (float)(qpz[pn] - tcz);
+                        pmn = fmax(pmn, ((double)fabsf(nx_[h]) + (double)fabsf(ny_[h]) + (double)fabsf(nz_[h])) * (1.0 + 1e-6));
+                    }
+                }
             }
-            // |fp32 coordinate - exact| <= |q - centre| 2^-24 per axis: within Ms * 2^-19 overall
+            const bool realq = active && a.fe.q_orig[vfull] != 0xffffffffu;
+            // |fp32 coordinate - exact| <= |p - centre| 2^-24 per axis: the seed-voxel distances are
+            // within Ms (the farthest seed plus the farthest voxel from the centre), their fp32
+            // error within Ms * 2^-19 overall
             const double pmq = realq ? ((double)fabsf(qfx) + (double)fabsf(qfy) + (double)fabsf(qfz)) * (1.0 + 1e-6) : 0.0;
-            const double Ms = 2.0 * uniform(wave_max(pmq)) + bhalf;
-            wave_lds_sync();
+            const double Ms = uniform(wave_max(fmax(pmq, pmn))) + uniform(wave_max(pmq)) + bhalf;
             float sd[KMAX];
 #pragma unroll
             for (int q = 0; q < KMAX; ++q) sd[q] = INFINITY;
-            for (int i = 0; i < nu; i += 2) {
-                const float2 X = *reinterpret_cast<const float2 *>(fbx + i);
-                const float2 Y = *reinterpret_cast<const float2 *>(fby + i);
-                const float2 Z = *reinterpret_cast<const float2 *>(fbz + i);
-                const f32x2 ex = qf2x - f32x2{X.x, X.y}, ey = qf2y - f32x2{Y.x, Y.y}, ez = qf2z - f32x2{Z.x, Z.y};
-                f32x2 s2 = ex * ex;
-                s2 = __builtin_elementwise_fma(ey, ey, s2);
-                s2 = __builtin_elementwise_fma(ez, ez, s2);
-                const float xs[2] = {s2.x, i + 1 < nu ? s2.y : INFINITY};
+            // two rounds through the candidate buffer (kCap = 128 entries): this blob and the one
+            // before it, then the one after it
 #pragma unroll
-                for (int u = 0; u < 2; ++u) {
-#pragma unroll
-                    for (int q = KMAX - 1; q > 0; --q) sd[q] = __builtin_amdgcn_fmed3f(sd[q - 1], sd[q], xs[u]);
-                    sd[0] = fminf(sd[0], xs[u]);
+            for (int round = 0; round < 2; ++round) {
+                int nu = 0;
+                auto put = [&](bool has, float x, float y, float z) {
+                    const unsigned long long m = __builtin_amdgcn_ballot_w64(has);
+                    if (has) {
+                        const int pos = nu + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                                            __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+                        fbx[pos] = x;
+                        fby[pos] = y;
+                        fbz[pos] = z;
+                    }
+                    nu += __builtin_popcountll(m);
+                };
+                if (round == 0) {
+                    put(realq, qfx, qfy, qfz);
+                    put(nreal[0], nx_[0], ny_[0], nz_[0]);
+                } else {
+                    put(nreal[1], nx_[1], ny_[1], nz_[1]);
                 }
+                wave_lds_sync();
+                for (int i = 0; i < nu; i += 2) {
+                    const float2 X = *reinterpret_cast<const float2 *>(fbx + i);
+                    const float2 Y = *reinterpret_cast<const float2 *>(fby + i);
+                    const float2 Z = *reinterpret_cast<const float2 *>(fbz + i);
+                    const f32x2 ex = qf2x - f32x2{X.x, X.y}, ey = qf2y - f32x2{Y.x, Y.y}, ez = qf2z - f32x2{Z.x, Z.y};
+                    f32x2 s2 = ex * ex;
+                    s2 = __builtin_elementwise_fma(ey, ey, s2);
+                    s2 = __builtin_elementwise_fma(ez, ez, s2);
+                    const float xs[2] = {s2.x, i + 1 < nu ? s2.y : INFINITY};
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+                        for (int q = KMAX - 1; q > 0; --q) sd[q] = __builtin_amdgcn_fmed3f(sd[q - 1], sd[q], xs[u]);
+                        sd[0] = fminf(sd[0], xs[u]);
+                    }
+                }
+                wave_lds_sync();  // the buffer is refilled next
             }
             float kth = sd[0];
 #pragma unroll
@@ -1272,11 +1322,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                     ub = sqrt_up(st2);
                 }
             }
-            // the per-lane bounds prune candidates; the gather radius still starts at the density
-            // radius (a Morton blob can be split, and its worst lane would set a huge radius)
-            seeded = false;
+            // the per-lane bounds prune candidates; the gather radius starts at the density radius
+            // (PTV_FILTER_SEEDED = 1: one pass at the wave's largest bound)
+            seeded = PTV_FILTER_SEEDED != 0;
             thr = dmin(kth2(), ub2);
-            wave_lds_sync();  // the gather reuses the candidate buffers
             stamp(t_seed);
         }
         double cpass = 0.0;
