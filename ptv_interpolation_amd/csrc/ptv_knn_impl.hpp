@@ -81,6 +81,23 @@ namespace ptv {
 // between passes; longer ones re-gather the records every pass (Sibson: four passes)
 #define PTV_KNN_KEEP_MAX 56
 #endif
+// unroll factors (same-box A/B, 512^3 / 5M, profiles/r06_ab/unroll_ab.txt): the k <= 8 seed
+// network's loop over pairs of seeds by 2 (headline main launch 14.09 -> 13.98 ms; the filter's
+// seed loop slower unrolled), the fp32 prefilter's loop over 4 candidates by 2 in the filter only
+#ifndef PTV_SEED_UNROLL
+#define PTV_SEED_UNROLL 2
+#endif
+#ifndef PTV_SEED_UNROLL_FILTER
+#define PTV_SEED_UNROLL_FILTER 1
+#endif
+#ifndef PTV_MASK_UNROLL
+#define PTV_MASK_UNROLL 1
+#endif
+#ifndef PTV_MASK_UNROLL_FILTER
+#define PTV_MASK_UNROLL_FILTER 2
+#endif
+#define PTV_PRAGMA_(x) _Pragma(#x)
+#define PTV_UNROLL(n) PTV_PRAGMA_(unroll n)
 #ifndef PTV_FILTER_SEEDED
 #define PTV_FILTER_SEEDED 0  // dev builds: 1 = the filter's first gather pass at its wave's largest seed bound
 #endif
@@ -1020,6 +1037,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                 float sd[KMAX];
 #pragma unroll
                 for (int q = 0; q < KMAX; ++q) sd[q] = INFINITY;
+                PTV_UNROLL(PTV_SEED_UNROLL)
                 for (int i = 0; i < nu; i += 2) {
                     const float2 X = *reinterpret_cast<const float2 *>(fbx + i);
                     const float2 Y = *reinterpret_cast<const float2 *>(fby + i);
@@ -1292,6 +1310,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                     put(nreal[1], nx_[1], ny_[1], nz_[1]);
                 }
                 wave_lds_sync();
+                PTV_UNROLL(PTV_SEED_UNROLL_FILTER)
                 for (int i = 0; i < nu; i += 2) {
                     const float2 X = *reinterpret_cast<const float2 *>(fbx + i);
                     const float2 Y = *reinterpret_cast<const float2 *>(fby + i);
@@ -1397,10 +1416,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                 const int ng = min(64, nbuf - g0);
                 // candidate g0 + j ends at bit nb - 1 - j (shift-in order keeps the loop rolled)
                 const int nb = (ng + 3) & ~3;
-                auto group_mask = [&]() -> unsigned long long {
-                unsigned long long m = 0ull;
-#pragma unroll 1
-                for (int i0 = 0; i0 < ng; i0 += 4) {
+                auto mask4 = [&](int i0) -> uint32_t {
                     // 4 candidates as two packed-fp32 pairs (v_pk_add / v_pk_mul / v_pk_fma);
                     // slots past nbuf hold stale values, their bits are cleared below
                     const float4 X = *reinterpret_cast<const float4 *>(fbx + g0 + i0);
@@ -1414,11 +1430,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                     s1 = __builtin_elementwise_fma(e1y, e1y, s1);
                     s0 = __builtin_elementwise_fma(e0z, e0z, s0);
                     s1 = __builtin_elementwise_fma(e1z, e1z, s1);
-                    const uint32_t b4 = ((s0.x <= thrf) ? 8u : 0u) | ((s0.y <= thrf) ? 4u : 0u) |
-                                        ((s1.x <= thrf) ? 2u : 0u) | ((s1.y <= thrf) ? 1u : 0u);
-                    m = (m << 4) | b4;
-                }
-                return m & ~((1ull << (nb - ng)) - 1ull);  // stale slots past nbuf
+                    return ((s0.x <= thrf) ? 8u : 0u) | ((s0.y <= thrf) ? 4u : 0u) |
+                           ((s1.x <= thrf) ? 2u : 0u) | ((s1.y <= thrf) ? 1u : 0u);
+                };
+                auto group_mask = [&]() -> unsigned long long {
+                    unsigned long long m = 0ull;
+                    if constexpr (MODE == kModeFilter) {
+                        // unrolled by 2 for the filter's long candidate streams (search 19.35 ->
+                        // 19.14 ms); rolled elsewhere (the headline +0.7 % unrolled)
+                        PTV_UNROLL(PTV_MASK_UNROLL_FILTER)
+                        for (int i0 = 0; i0 < ng; i0 += 4) m = (m << 4) | mask4(i0);
+                    } else {
+                        PTV_UNROLL(PTV_MASK_UNROLL)
+                        for (int i0 = 0; i0 < ng; i0 += 4) m = (m << 4) | mask4(i0);
+                    }
+                    return m & ~((1ull << (nb - ng)) - 1ull);  // stale slots past nbuf
                 };
                 unsigned long long m = group_mask();
                 const double4 *gbuf = buf + g0 + nb - 64;  // bit position p <-> gbuf[63 - p]
