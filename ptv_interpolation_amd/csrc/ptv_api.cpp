@@ -62,6 +62,14 @@ struct ptv_ctx {
     int cdk_n[3] = {0, 0, 0};
     bool cmap_valid = false;
     std::vector<double> ckey, ckey_new;
+    // the speculative reuse of the cached map (no host synchronisation before the gated launch): the
+    // host part of the key, the data part on the device, the kept count and bounding box of the
+    // last proven culled call
+    std::vector<double> ckey_host;
+    DevBuf<double> ckey_dev;
+    bool ckept_valid = false;
+    int64_t ckept = 0;
+    double cbbox[6] = {0, 0, 0, 0, 0, 0};
     DevBuf<uint32_t> slots;                                      // local RBF: chunk k-NN slots
     DevBuf<int> rbf_pw, rbf_status;                              // monomial exponents, singular count
     DevBuf<uint32_t> rbf_nslist;                                 // local RBF: voxels k_rbf_ns hands over
@@ -211,6 +219,7 @@ int ptv_free(ptv_ctx *c) {
     c->cdk.release();
     c->ccols.release();
     c->cfp.release();
+    c->ckey_dev.release();
     c->ckeys.release();
     c->slots.release();
     c->rbf_pw.release();
@@ -742,27 +751,45 @@ int run_knn_auto(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const pt
     PTV_TRY(c->cfp.ensure(nkey));
     PTV_TRY(launch_fingerprint(src, n, c->cfp.p, s));
     PTV_TRY(launch_concat3(ax, (int)g->nx, ay, (int)g->ny, az, (int)g->nz, c->cfp.p + nfp, s));
-    std::vector<double> &key = c->ckey_new;
-    key.assign(nkey, 0.0);
-    PTV_HIP(hipMemcpyAsync(key.data(), c->cfp.p, nkey * sizeof(double), hipMemcpyDeviceToHost, s));
-    PTV_HIP(hipStreamSynchronize(s));
+    // the host part of the key: the arrays, n, the grid, the slab, k, method
+    std::vector<double> hkey;
     for (const void *q : {(const void *)p->x, (const void *)p->y, (const void *)p->z, (const void *)p->u,
                           (const void *)p->v, (const void *)p->w, (const void *)ax, (const void *)ay,
                           (const void *)az}) {
         uint64_t bits = (uint64_t)(uintptr_t)q;
         double d;
         std::memcpy(&d, &bits, sizeof(d));
-        key.push_back(d);
+        hkey.push_back(d);
     }
     for (int64_t v : {n, g->nx, g->ny, g->nz, g->z_begin, g->z_end, (int64_t)prm->k, (int64_t)prm->method,
                       (int64_t)prm->lattice_bounds})
-        key.push_back((double)v);
-    // bitwise comparison (a NaN fingerprint value never matches itself otherwise)
-    bool use_map = c->cmap_valid && c->ckey.size() == key.size() &&
-                   std::memcmp(c->ckey.data(), key.data(), key.size() * sizeof(double)) == 0;
+        hkey.push_back((double)v);
+    const bool host_match = c->cmap_valid && c->ckey_host.size() == hkey.size() &&
+                            std::memcmp(c->ckey_host.data(), hkey.data(), hkey.size() * sizeof(double)) == 0 &&
+                            c->ckey.size() == nkey + hkey.size();
+    // speculative: a proven culled call already ran with this host key, so cull with the map at once and
+    // let the device compare the data part (fingerprint + axis values) and the kept count, folded into
+    // the gate of the main launch; the host reads the gate once, after it (no synchronisation before)
+    bool spec = host_match && c->ckept_valid;
+    std::vector<double> &key = c->ckey_new;
+    auto read_key = [&]() -> int {
+        key.assign(nkey, 0.0);
+        PTV_HIP(hipMemcpyAsync(key.data(), c->cfp.p, nkey * sizeof(double), hipMemcpyDeviceToHost, s));
+        PTV_HIP(hipStreamSynchronize(s));
+        key.insert(key.end(), hkey.begin(), hkey.end());
+        return PTV_OK;
+    };
+    bool use_map = spec;
+    if (!spec) {
+        PTV_TRY(read_key());
+        // bitwise comparison (a NaN fingerprint value never matches itself otherwise)
+        use_map = c->cmap_valid && c->ckey.size() == key.size() &&
+                  std::memcmp(c->ckey.data(), key.data(), key.size() * sizeof(double)) == 0;
+    }
     if (dev_knob("PTV_DBG_CULL"))
-        std::fprintf(stderr, "[cull] slab [%lld, %lld) n %lld: cached map %d, key match %d\n", (long long)g->z_begin,
-                     (long long)g->z_end, (long long)n, (int)c->cmap_valid, (int)use_map);
+        std::fprintf(stderr, "[cull] slab [%lld, %lld) n %lld: cached map %d, key match %d, speculative %d\n",
+                     (long long)g->z_begin, (long long)g->z_end, (long long)n, (int)c->cmap_valid, (int)use_map,
+                     (int)spec);
     for (int attempt = 0; attempt < 2; ++attempt) {
         KnnLaunch kl;
         Binned b{};
@@ -784,6 +811,25 @@ int run_knn_auto(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const pt
             PTV_HIP(hipEventRecord(c->ev_cull0, s));
             PTV_TRY(launch_cull(src, n, az, (int)g->z_begin, (int)g->z_end, 0.0, c->cull_win.p, c->cull_cnt.p,
                                 c->cull_mask.p, dst, nullptr, s, &used));
+            if (spec) {
+                // the cached kept count and bounding box (the same particles give the same), checked on
+                // the device: a mismatch fails the gate and the call reruns with every particle binned
+                PTV_TRY(c->halo_need.ensure(1));
+                PTV_HIP(hipMemsetAsync(c->halo_need.p, 0, sizeof(unsigned long long), s));
+                PTV_TRY(launch_key_check(c->cfp.p, c->ckey_dev.p, (int)nkey, c->cull_cnt.p + nb, (uint32_t)c->ckept,
+                                         c->halo_need.p, s));
+                PTV_HIP(hipEventRecord(c->ev_cull1, s));
+                std::memcpy(c->h_bbox, c->cbbox, sizeof(c->cbbox));
+                pe = ptv_particles{c->ckept, dst[0], dst[1], dst[2], dst[3], dst[4], dst[5]};
+                culled = true;
+                c->cull_timed = true;
+            }
+        }
+        if (use_map && !spec) {
+            const size_t nb = cull_blocks(n);
+            double *dst[6];
+            for (int a = 0; a < 6; ++a) dst[a] = c->cull[a].p;
+            uint32_t *h_total = reinterpret_cast<uint32_t *>(c->h_misc);
             PTV_TRY(c->bbox_part.ensure(6 * 1024));
             PTV_TRY(c->bbox_out.ensure(8));
             const double *kp[3] = {dst[0], dst[1], dst[2]};
@@ -856,7 +902,8 @@ int run_knn_auto(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const pt
             // cached map was built from the bounds of the call that binned every particle (widened by
             // kCullMapSlack), so bounds of the kept particles within half that of the cached ones
             // prove that the map holds every particle a slab voxel can need
-            PTV_TRY(launch_bounds_within(kl.cb.dk, c->cdk.p, nlp, 1.0 + 0.5 * kCullMapSlack, c->halo_need.p, s));
+            PTV_TRY(launch_bounds_within(kl.cb.dk, c->cdk.p, nlp, 1.0 + 0.5 * kCullMapSlack, c->halo_need.p, s,
+                                         !spec));
             kl.gate = c->halo_need.p;
             kl.gate_halo = 0.0;
             PTV_HIP(hipEventRecord(c->ev_main0, s));
@@ -879,6 +926,10 @@ int run_knn_auto(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const pt
             c->cmap_geo = geo;
             c->cmap_valid = true;
             c->ckey = key;
+            c->ckey_host = hkey;
+            PTV_TRY(c->ckey_dev.ensure(nkey));
+            PTV_HIP(hipMemcpyAsync(c->ckey_dev.p, c->cfp.p, nkey * sizeof(double), hipMemcpyDeviceToDevice, s));
+            c->ckept_valid = false;
             if (st) *st = c->last;
             return PTV_OK;
         }
@@ -890,12 +941,23 @@ int run_knn_auto(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const pt
                          (unsigned long long)c->h_misc[1]);
         if (c->h_misc[1] == 0ull) {  // proven: the gated launch wrote every output
             c->last.halo_required = 0.0;
+            if (!spec) {  // later calls with this key may run speculatively
+                c->ckept = pe.n;
+                std::memcpy(c->cbbox, c->h_bbox, sizeof(c->cbbox));
+                c->ckept_valid = true;
+            }
             if (st) *st = c->last;
             return PTV_OK;
         }
-        // not proven (the particles changed under the same arrays and fingerprint): no outputs were
-        // written; again with every particle binned, which refreshes the map
+        // not proven (the particles changed under the same arrays and fingerprint, or under a
+        // speculative reuse the data key or kept count differed): no outputs were written; again with
+        // every particle binned, which refreshes the map
         c->cmap_valid = false;
+        c->ckept_valid = false;
+        if (spec) {
+            spec = false;
+            PTV_TRY(read_key());  // the map built next is keyed by this call's data
+        }
         use_map = false;
     }
     set_error("slab cull map: unreachable retry state");

@@ -598,9 +598,29 @@ __global__ __launch_bounds__(256) void k_bounds_within(const double *__restrict_
         atomicMax(fail, (unsigned long long)__double_as_longlong(INFINITY));
 }
 
+// the cached cull map's speculative reuse: *fail = +inf's bits unless key[0..n) equals ref bitwise and
+// the kept count equals the cached one (atomicMax: it only ever raises the word)
+__global__ __launch_bounds__(256) void k_key_check(const double *__restrict__ key, const double *__restrict__ ref,
+                                                   int n, const uint32_t *__restrict__ count, uint32_t expect,
+                                                   unsigned long long *__restrict__ fail) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const bool bad = (i < n && __double_as_longlong(key[i]) != __double_as_longlong(ref[i])) ||
+                     (i == 0 && *count != expect);
+    if (__builtin_amdgcn_ballot_w64(bad) != 0 && (threadIdx.x & 63) == 0)
+        atomicMax(fail, (unsigned long long)__double_as_longlong(INFINITY));
+}
+
+int launch_key_check(const double *key, const double *ref, int n, const uint32_t *count, uint32_t expect,
+                     unsigned long long *fail, hipStream_t s) {
+    hipLaunchKernelGGL(k_key_check, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, key, ref, n, count, expect,
+                       fail);
+    PTV_HIP(hipGetLastError());
+    return PTV_OK;
+}
+
 int launch_bounds_within(const double *dk, const double *ref, long long n, double factor, unsigned long long *fail,
-                         hipStream_t s) {
-    PTV_HIP(hipMemsetAsync(fail, 0, sizeof(unsigned long long), s));
+                         hipStream_t s, bool reset) {
+    if (reset) PTV_HIP(hipMemsetAsync(fail, 0, sizeof(unsigned long long), s));
     hipLaunchKernelGGL(k_bounds_within, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, dk, ref, n, factor, fail);
     PTV_HIP(hipGetLastError());
     return PTV_OK;

@@ -47,7 +47,10 @@ int launch_cull(const double *const src[6], int64_t n, const double *az, int z0,
 // convention).
 // *fail = 0 when dk[i] <= ref[i] * factor for every i < n, else +inf's bits (the cached cull map's proof)
 int launch_bounds_within(const double *dk, const double *ref, long long n, double factor, unsigned long long *fail,
-                         hipStream_t s);
+                         hipStream_t s, bool reset = true);
+// *fail raised to +inf's bits unless key == ref (n doubles, bitwise) and *count == expect
+int launch_key_check(const double *key, const double *ref, int n, const uint32_t *count, uint32_t expect,
+                     unsigned long long *fail, hipStream_t s);
 int launch_cull_need(const double *lax, const double *lay, const double *laz, const int n[3], const double *dk,
                      double mg, double slack, const CullMap &m, double *top, double *bot, double *cols,
                      unsigned long long *keys, const CullMap *used, unsigned long long *fail, hipStream_t s);

@@ -1,13 +1,15 @@
 """Print the kernel timeline of the last step of a rocprofv3 --kernel-trace run (dev tool).
 
-usage: python tools/trace_step.py <trace dir>   (a step starts at each k_bbox dispatch)"""
+usage: python tools/trace_step.py <trace dir>   (a step starts at each k_fingerprint, or k_bbox, dispatch)"""
 import csv, glob, sys
 
 rows = []
 for f in glob.glob(f"{sys.argv[1]}/**/*kernel_trace.csv", recursive=True):
     rows += list(csv.DictReader(open(f)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-starts = [i for i, r in enumerate(rows) if "k_bbox(" in r["Kernel_Name"]]
+# a step starts at its first kernel: k_fingerprint for a slab-culled call (the cull map's key), else k_bbox
+mark = "k_fingerprint(" if any("k_fingerprint(" in r["Kernel_Name"] for r in rows) else "k_bbox("
+starts = [i for i, r in enumerate(rows) if mark in r["Kernel_Name"]]
 step = rows[starts[-2]:starts[-1]] if len(starts) > 1 else rows
 t0 = int(step[0]["Start_Timestamp"])
 for r in step:
