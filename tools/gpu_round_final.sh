@@ -18,4 +18,7 @@ if [ -z "$SKIP_TESTS" ]; then
 fi
 bash tools/collect_profiles.sh ${tag} || exit 1
 tail -4 profiles/${tag}_summary.txt
+# profiles/ on the box is not merged back: copy what collect_profiles wrote
+mkdir -p gpurun_out/profiles_box
+cp profiles/traffic_${tag}.json profiles/${tag}_summary.txt profiles/${tag}_kernel_stats.csv gpurun_out/profiles_box/
 [ -n "$SKIP_LINES" ] || bash tools/gpu_lines.sh ${tag}
