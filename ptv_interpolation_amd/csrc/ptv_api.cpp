@@ -46,6 +46,8 @@ struct ptv_ctx {
     DevBuf<double> rbf_huge;  // k_rbf_huge's per-workgroup slices (m > 128)
     DevBuf<uint8_t> mask;
     DevBuf<uint32_t> code, perm, count, start, scanp;
+    DevBuf<uint32_t> bin_keys;                                   // sort-based binning: sorted cell codes
+    DevBuf<uint8_t> bin_temp;                                    //   and the radix sort's scratch
     DevBuf<double4> prec, pval;
     DevBuf<double> bbox_part, bbox_out;
     DevBuf<unsigned long long> dbg;
@@ -199,6 +201,8 @@ int ptv_free(ptv_ctx *c) {
     c->code.release();
     c->perm.release();
     c->count.release();
+    c->bin_keys.release();
+    c->bin_temp.release();
     c->start.release();
     c->scanp.release();
     c->prec.release();
@@ -312,6 +316,9 @@ constexpr long long kLatticeSplitDiv = 128;
 // memset once per level): 64 MiB = 512 blocks at KMAX 8, 32 at 128; the measured win came from the
 // first ~64 blocks, while nb / 128 at 2048^3 would be ~4300 blocks (0.56 GB at k = 8, 9 GB at 127)
 constexpr size_t kLatticeSplitBytesMax = 64ULL << 20;
+// binning: the radix sort above this many particles, the atomic counting sort below (crossover
+// ~2.6M from the two measured points, profiles/r06_ab/bin_sort_ab.txt)
+constexpr int64_t kBinSortMinParticles = 2500000;
 // relative widening of the cached slab cull map over the need it was built from
 constexpr double kCullMapSlack = 1e-6;
 
@@ -509,8 +516,22 @@ int prepare(ptv_ctx *c, const ptv_particles *p, const ptv_grid *g, const SearchP
     PTV_TRY(c->start.ensure(m + 1));
     PTV_TRY(c->scanp.ensure(scan_partials_needed(m) + 1));
     const double *pv[3] = {p->u, p->v, p->w};
+    // sort-based binning (a stable radix sort of (cell, index) pairs) from kBinSortMinParticles:
+    // 512^3 / 5M binning 0.81 -> 0.68 ms against the atomic histogram + scatter + in-cell sort,
+    // the 0.73M particles of share 2/8 0.134 -> 0.22 ms (profiles/r06_ab/bin_sort_ab.txt)
+    BinSortScratch ss;
+    const char *bs = dev_knob("PTV_BIN_SORT");  // dev knob: 0 = the atomic counting sort, 1 = the sort
+    const bool use_sort = bs ? bs[0] == '1' : n >= kBinSortMinParticles;
+    const size_t tb = use_sort ? bin_sort_temp_bytes(n, m) : 0;
+    if (tb > 0) {
+        PTV_TRY(c->bin_keys.ensure((size_t)n));
+        PTV_TRY(c->bin_temp.ensure(std::max<size_t>(tb, 1)));
+        ss.keys = c->bin_keys.p;
+        ss.temp = c->bin_temp.p;
+        ss.temp_bytes = tb;
+    }
     PTV_TRY(launch_bin(cg, pp, pv, n, c->code.p, c->perm.p, c->count.p, c->start.p, c->scanp.p, c->prec.p,
-                       c->pval.p, s));
+                       c->pval.p, s, &ss));
     PTV_HIP(hipEventRecord(c->ev_bin1, s));
 
     // Seed records for the main launch (the finest level's k-NN lists) pay for the pair lists (k <=

@@ -13,6 +13,7 @@
 //   gather      AoS records for the scalar-load k-NN kernel:
 //                 prec[slot] = (x, y, z, id), pval[slot] = (u, v, w, 0)
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -664,9 +665,80 @@ int launch_fingerprint(const double *const src[6], int64_t n, double *out, hipSt
     return PTV_OK;
 }
 
+// ---------------------------------------------------------------------------
+// sort-based binning: cell codes without atomics, a stable radix sort of (code, index) pairs
+// (in-cell order = ascending original index, as k_seg_sort makes it), cell starts by binary
+// search, the inverse permutation, then k_place
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_cell_key(CellGrid cg, const double *__restrict__ x,
+                                                  const double *__restrict__ y, const double *__restrict__ z,
+                                                  int64_t n, uint32_t *__restrict__ code, uint32_t *__restrict__ idx) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int cx = cell_coord(x[i], cg.o[0], cg.ic[0], cg.nc[0]);
+    const int cy = cell_coord(y[i], cg.o[1], cg.ic[1], cg.nc[1]);
+    const int cz = cell_coord(z[i], cg.o[2], cg.ic[2], cg.nc[2]);
+    code[i] = (uint32_t)(((long long)cz * cg.nc[1] + cy) * cg.nc[0] + cx);
+    idx[i] = (uint32_t)i;
+}
+
+// start[c] = first sorted position whose code is >= c (c in [0, m]), and inv[perm[j]] = j
+__global__ __launch_bounds__(256) void k_sorted_starts(const uint32_t *__restrict__ skey, int64_t n, size_t m,
+                                                       const uint32_t *__restrict__ perm, uint32_t *__restrict__ start,
+                                                       uint32_t *__restrict__ inv) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < n) inv[perm[t]] = (uint32_t)t;
+    if (t > (int64_t)m) return;
+    int64_t lo = 0, hi = n;  // first j with skey[j] >= t
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if ((int64_t)skey[mid] < t) lo = mid + 1;
+        else hi = mid;
+    }
+    start[t] = (uint32_t)lo;
+}
+
+static int cell_key_bits(size_t m) {
+    int b = 1;
+    while (b < 32 && ((size_t)1 << b) < m) ++b;
+    return b;
+}
+
+size_t bin_sort_temp_bytes(int64_t n, size_t m) {
+    size_t tb = 0;
+    if (hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                           (const uint32_t *)nullptr, (uint32_t *)nullptr, (int)n, 0,
+                                           cell_key_bits(m)) != hipSuccess)
+        return 0;
+    return tb;
+}
+
+static int launch_bin_sort(const CellGrid &cg, const double *const px[3], const double *const pv[3], int64_t n,
+                           uint32_t *d_code, uint32_t *d_perm, uint32_t *d_start, double4 *d_prec,
+                           double4 *d_pval, const BinSortScratch &ss, hipStream_t s) {
+    const size_t m = (size_t)cg.ncells;
+    const int nb = (int)((n + 255) / 256);
+    uint32_t *d_idx = d_code + n;
+    hipLaunchKernelGGL(k_cell_key, dim3(nb), dim3(256), 0, s, cg, px[0], px[1], px[2], n, d_code, d_idx);
+    size_t tb = ss.temp_bytes;
+    PTV_HIP(hipcub::DeviceRadixSort::SortPairs(ss.temp, tb, (const uint32_t *)d_code, ss.keys, (const uint32_t *)d_idx,
+                                               d_perm, (int)n, 0, cell_key_bits(m), s));
+    const int64_t nt = std::max<int64_t>(n, (int64_t)m + 1);
+    // d_code is dead after the sort: it holds the inverse permutation from here on
+    hipLaunchKernelGGL(k_sorted_starts, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s,
+                       (const uint32_t *)ss.keys, n, m, (const uint32_t *)d_perm, d_start, d_code);
+    hipLaunchKernelGGL(k_place, dim3(nb), dim3(256), 0, s, (const uint32_t *)d_code, n, px[0], px[1], px[2],
+                       pv[0], pv[1], pv[2], d_prec, d_pval);
+    PTV_HIP(hipGetLastError());
+    return PTV_OK;
+}
+
 int launch_bin(const CellGrid &cg, const double *const px[3], const double *const pv[3], int64_t n,
                uint32_t *d_code, uint32_t *d_perm, uint32_t *d_count, uint32_t *d_start,
-               uint32_t *d_scan_partials, double4 *d_prec, double4 *d_pval, hipStream_t s) {
+               uint32_t *d_scan_partials, double4 *d_prec, double4 *d_pval, hipStream_t s,
+               const BinSortScratch *ss) {
+    if (ss != nullptr && ss->keys != nullptr && ss->temp != nullptr)
+        return launch_bin_sort(cg, px, pv, n, d_code, d_perm, d_start, d_prec, d_pval, *ss, s);
     const size_t m = (size_t)cg.ncells;
     PTV_HIP(hipMemsetAsync(d_count, 0, m * sizeof(uint32_t), s));
     const int nb = (int)((n + 255) / 256);

@@ -15,9 +15,18 @@ int launch_bbox(const double *const px[3], int64_t n, const double *const qa[3],
 // Counting-sort the particles into linear-order cells (deterministic order
 // inside each cell: ascending original index).  Scratch buffers must hold
 // 2n (code), n (perm) and ncells (+1) entries (count, start).
+// With a BinSortScratch (keys: n entries, temp: bin_sort_temp_bytes(n, ncells)) the binning is a
+// stable radix sort of (cell, index) pairs instead (no per-particle atomics; same result).
+struct BinSortScratch {
+    uint32_t *keys = nullptr;
+    void *temp = nullptr;
+    size_t temp_bytes = 0;
+};
+size_t bin_sort_temp_bytes(int64_t n, size_t m);
 int launch_bin(const CellGrid &cg, const double *const px[3], const double *const pv[3], int64_t n,
                uint32_t *d_code, uint32_t *d_perm, uint32_t *d_count, uint32_t *d_start,
-               uint32_t *d_scan_partials, double4 *d_prec, double4 *d_pval, hipStream_t s);
+               uint32_t *d_scan_partials, double4 *d_prec, double4 *d_pval, hipStream_t s,
+               const BinSortScratch *ss = nullptr);
 
 size_t scan_partials_needed(size_t m);
 

@@ -46,7 +46,7 @@ def kernels(obj):
 def main():
     flt = sys.argv[1] if len(sys.argv) > 1 else ""
     rows = []
-    for obj in sorted(glob.glob(os.path.join(ROOT, "ptv_interpolation_amd", "csrc", "_build", "*.o"))):
+    for obj in sorted(glob.glob(os.path.join(ROOT, "ptv_interpolation_amd", "csrc", os.environ.get("PTV_RES_BUILD", "_build"), "*.o"))):
         for r in kernels(obj):
             rows.append((os.path.basename(obj),) + r)
     names = demangle([r[1] for r in rows])
