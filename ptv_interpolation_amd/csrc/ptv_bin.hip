@@ -682,20 +682,40 @@ __global__ __launch_bounds__(256) void k_cell_key(CellGrid cg, const double *__r
     idx[i] = (uint32_t)i;
 }
 
-// start[c] = first sorted position whose code is >= c (c in [0, m]), and inv[perm[j]] = j
-__global__ __launch_bounds__(256) void k_sorted_starts(const uint32_t *__restrict__ skey, int64_t n, size_t m,
-                                                       const uint32_t *__restrict__ perm, uint32_t *__restrict__ start,
-                                                       uint32_t *__restrict__ inv) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < n) inv[perm[t]] = (uint32_t)t;
-    if (t > (int64_t)m) return;
-    int64_t lo = 0, hi = n;  // first j with skey[j] >= t
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if ((int64_t)skey[mid] < t) lo = mid + 1;
-        else hi = mid;
+// inv[perm[j]] = j (the placement pass writes each particle's records at its slot), and
+// start[c] = first sorted position whose code is >= c, c in [0, m]: thread j at a code change
+// (codes c' < c at j - 1, j) writes the start of cells (c', c] -- up to kStartGap of them (the
+// pack's solid spheres leave runs of hundreds of empty x-thin cells); a longer run of empty cells
+// raises *flag and k_start_fixup then binary-searches every cell
+constexpr int kStartGap = 1 << 16;
+__global__ __launch_bounds__(256) void k_sorted_starts(const uint32_t *__restrict__ skey, const uint32_t *__restrict__ perm,
+                                                       int64_t n, size_t m, uint32_t *__restrict__ start,
+                                                       uint32_t *__restrict__ inv, uint32_t *__restrict__ flag) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j > n) return;
+    if (j < n) inv[perm[j]] = (uint32_t)j;
+    const int64_t prev = j == 0 ? -1 : (int64_t)skey[j - 1];
+    const int64_t cur = j == n ? (int64_t)m : (int64_t)skey[j];
+    if (cur - prev > kStartGap) {
+        atomicOr(flag, 1u);
+        return;
     }
-    start[t] = (uint32_t)lo;
+    for (int64_t c = prev + 1; c <= cur; ++c) start[c] = (uint32_t)j;
+}
+
+__global__ __launch_bounds__(256) void k_start_fixup(const uint32_t *__restrict__ skey, int64_t n, size_t m,
+                                                     uint32_t *__restrict__ start, const uint32_t *__restrict__ flag) {
+    if (*flag == 0u) return;
+    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c <= (int64_t)m;
+         c += (int64_t)gridDim.x * blockDim.x) {
+        int64_t lo = 0, hi = n;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if ((int64_t)skey[mid] < c) lo = mid + 1;
+            else hi = mid;
+        }
+        start[c] = (uint32_t)lo;
+    }
 }
 
 static int cell_key_bits(size_t m) {
@@ -714,8 +734,8 @@ size_t bin_sort_temp_bytes(int64_t n, size_t m) {
 }
 
 static int launch_bin_sort(const CellGrid &cg, const double *const px[3], const double *const pv[3], int64_t n,
-                           uint32_t *d_code, uint32_t *d_perm, uint32_t *d_start, double4 *d_prec,
-                           double4 *d_pval, const BinSortScratch &ss, hipStream_t s) {
+                           uint32_t *d_code, uint32_t *d_perm, uint32_t *d_count, uint32_t *d_start,
+                           double4 *d_prec, double4 *d_pval, const BinSortScratch &ss, hipStream_t s) {
     const size_t m = (size_t)cg.ncells;
     const int nb = (int)((n + 255) / 256);
     uint32_t *d_idx = d_code + n;
@@ -723,10 +743,13 @@ static int launch_bin_sort(const CellGrid &cg, const double *const px[3], const 
     size_t tb = ss.temp_bytes;
     PTV_HIP(hipcub::DeviceRadixSort::SortPairs(ss.temp, tb, (const uint32_t *)d_code, ss.keys, (const uint32_t *)d_idx,
                                                d_perm, (int)n, 0, cell_key_bits(m), s));
-    const int64_t nt = std::max<int64_t>(n, (int64_t)m + 1);
-    // d_code is dead after the sort: it holds the inverse permutation from here on
-    hipLaunchKernelGGL(k_sorted_starts, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s,
-                       (const uint32_t *)ss.keys, n, m, (const uint32_t *)d_perm, d_start, d_code);
+    // d_code is dead after the sort: it holds the inverse permutation from here on; the flag word
+    // is the first of the (unused) count buffer
+    PTV_HIP(hipMemsetAsync(d_count, 0, sizeof(uint32_t), s));
+    hipLaunchKernelGGL(k_sorted_starts, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, s,
+                       (const uint32_t *)ss.keys, (const uint32_t *)d_perm, n, m, d_start, d_code, d_count);
+    hipLaunchKernelGGL(k_start_fixup, dim3(1024), dim3(256), 0, s, (const uint32_t *)ss.keys, n, m, d_start,
+                       (const uint32_t *)d_count);
     hipLaunchKernelGGL(k_place, dim3(nb), dim3(256), 0, s, (const uint32_t *)d_code, n, px[0], px[1], px[2],
                        pv[0], pv[1], pv[2], d_prec, d_pval);
     PTV_HIP(hipGetLastError());
@@ -738,7 +761,7 @@ int launch_bin(const CellGrid &cg, const double *const px[3], const double *cons
                uint32_t *d_scan_partials, double4 *d_prec, double4 *d_pval, hipStream_t s,
                const BinSortScratch *ss) {
     if (ss != nullptr && ss->keys != nullptr && ss->temp != nullptr)
-        return launch_bin_sort(cg, px, pv, n, d_code, d_perm, d_start, d_prec, d_pval, *ss, s);
+        return launch_bin_sort(cg, px, pv, n, d_code, d_perm, d_count, d_start, d_prec, d_pval, *ss, s);
     const size_t m = (size_t)cg.ncells;
     PTV_HIP(hipMemsetAsync(d_count, 0, m * sizeof(uint32_t), s));
     const int nb = (int)((n + 255) / 256);

@@ -207,3 +207,49 @@ def test_full_size_sampled(ctx, method, G, N, k):
             print(f"sibson k={k} {G}^3/{N} component {c}: normwise {err:.2e}, "
                   f"bit-identical {np.mean(got[:, c] == ref[:, c]):.4%}")
             assert err <= TOL
+
+
+@pytest.mark.timeout(300)
+def test_sort_binning_clustered_vs_oracle(ctx):
+    """The sort-based binning (from 2.5M particles, ptv_bin.hip k_cell_key / radix sort /
+    k_sorted_starts): half of 2.6M particles uniform, half in a cluster 1/64 of a voxel wide, so
+    that cells hold up to ~10^5 particles (the cell-start walk's binary-search fallback) next to
+    long runs of empty cells.  IDW k = 8 on a 64^3 grid: 20k voxels bit-exact against the oracle,
+    and a z-slab call equal to the whole-grid planes."""
+    from oracle import cpu_ref
+
+    rng = np.random.default_rng(77)
+    G, half = 64, 1_300_000
+    P = np.concatenate([rng.uniform(0, G - 1, (half, 3)), 30.0 + rng.uniform(0, 1 / 64, (half, 3))])
+    Q = rng.standard_normal((2 * half, 3))
+    ax = np.arange(G, dtype=np.float64)
+    U, V, W = ctx.interp_knn(P, Q, axes=(ax, ax, ax), k=8)
+    idx = rng.integers(0, G, size=(20000, 3))
+    idx[:500] = rng.integers(29, 33, size=(500, 3))  # voxels next to the cluster
+    q = np.stack([ax[idx[:, 2]], ax[idx[:, 1]], ax[idx[:, 0]]], -1)
+    ref = cpu_ref.interp_points(P, Q, q, "idw", 8, 2.0)
+    got = np.stack([A[idx[:, 0], idx[:, 1], idx[:, 2]] for A in (U, V, W)], -1)
+    assert np.array_equal(got, ref)
+    part = ctx.interp_knn(P, Q, axes=(ax, ax, ax), k=8, z_range=(20, 40))
+    for a, b in zip(part, (U, V, W)):
+        assert np.array_equal(a, b[20:40])
+
+
+@pytest.mark.timeout(300)
+def test_sort_binning_empty_runs_vs_oracle(ctx):
+    """Sort-based binning where the cell grid (over particles + grid) has runs of more than 256
+    empty cells (the cell-start pass's binary-search fix-up): 2.6M particles in one corner
+    eighth of a 64^3 grid; 10k voxels, most of them far from every particle, bit-exact."""
+    from oracle import cpu_ref
+
+    rng = np.random.default_rng(78)
+    G = 64
+    P = rng.uniform(0, 16, (2_600_000, 3))
+    Q = rng.standard_normal((len(P), 3))
+    ax = np.arange(G, dtype=np.float64)
+    U, V, W = ctx.interp_knn(P, Q, axes=(ax, ax, ax), k=8)
+    idx = rng.integers(0, G, size=(10000, 3))
+    q = np.stack([ax[idx[:, 2]], ax[idx[:, 1]], ax[idx[:, 0]]], -1)
+    ref = cpu_ref.interp_points(P, Q, q, "idw", 8, 2.0)
+    got = np.stack([A[idx[:, 0], idx[:, 1], idx[:, 2]] for A in (U, V, W)], -1)
+    assert np.array_equal(got, ref)
