@@ -2,16 +2,22 @@
 //
 // Replaces the role of the per-call cKDTree build in the reference
 // (interpolator.py:90 and :132, scipy KDTree(points), leafsize 10): particles
-// are counting-sorted into a uniform cell grid in linear (z, y, x) order, so
-// that every x-run of cells in a row is one contiguous particle range.
+// are sorted into a uniform cell grid in linear (z, y, x) order, so that every
+// x-run of cells in a row is one contiguous particle range.
 //
 //   bbox        per-axis min/max of particles and queries (grid-stride, LDS reduce)
-//   cell_code   linear cell id per particle + atomic histogram
-//   scan        exclusive prefix sum of the cell histogram (3-phase, 4096 cells/block)
-//   scatter     particle -> slot (atomic fill from the back of each cell)
-//   seg_sort    ascending original index inside each cell (deterministic order)
-//   gather      AoS records for the scalar-load k-NN kernel:
-//                 prec[slot] = (x, y, z, id), pval[slot] = (u, v, w, 0)
+//   from 2.5M particles (launch_bin_sort):
+//     cell_key      linear cell id per particle, no atomics
+//     radix sort    stable hipCUB sort of (cell, index) pairs: in-cell order = index order
+//     sorted_starts inverse permutation + cell starts at the code changes (fix-up for
+//                   runs of > 65536 empty cells)
+//   below (the atomic counting sort):
+//     cell_code   linear cell id per particle + atomic histogram
+//     scan        exclusive prefix sum of the cell histogram (3-phase, 4096 cells/block)
+//     scatter     particle -> slot (atomic fill from the back of each cell)
+//     seg_sort    ascending original index inside each cell (deterministic order)
+//   place       AoS records for the scalar-load k-NN kernel, in original order through
+//               the inverse permutation: prec[slot] = (x, y, z, id), pval[slot] = (u, v, w, 0)
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 

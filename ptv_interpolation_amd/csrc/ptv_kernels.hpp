@@ -12,7 +12,7 @@ int launch_bbox(const double *const px[3], int64_t n, const double *const qa[3],
                 double *d_partials, int max_blocks, double *d_out6, hipStream_t s,
                 const uint32_t *d_n = nullptr);  // d_n: the particle count on the device (<= n)
 
-// Counting-sort the particles into linear-order cells (deterministic order
+// Sort the particles into linear-order cells (deterministic order
 // inside each cell: ascending original index).  Scratch buffers must hold
 // 2n (code), n (perm) and ncells (+1) entries (count, start).
 // With a BinSortScratch (keys: n entries, temp: bin_sort_temp_bytes(n, ncells)) the binning is a

@@ -9,7 +9,7 @@ tag=${1:-r05}
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 mkdir -p gpurun_out
 if [ -z "$SKIP_TESTS" ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > gpurun_out/${tag}_tests.log 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -q -rA -s --timeout 300 --timeout-method thread > gpurun_out/${tag}_tests.log 2>&1
   rc=$?
   tail -3 gpurun_out/${tag}_tests.log
   if [ $rc -ne 0 ]; then grep -E "FAILED|Error" gpurun_out/${tag}_tests.log | head -20; exit $rc; fi
