@@ -87,6 +87,9 @@ namespace ptv {
 #ifndef PTV_SEED_UNROLL
 #define PTV_SEED_UNROLL 2
 #endif
+#ifndef PTV_K1_BROADCAST_SEEDS
+#define PTV_K1_BROADCAST_SEEDS 1  // one-slot list: corner seeds by lane broadcast (no LDS hash)
+#endif
 #ifndef PTV_SEED_UNROLL_FILTER
 #define PTV_SEED_UNROLL_FILTER 1
 #endif
@@ -998,6 +1001,53 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
         const f32x2 qf2x = {qfx, qfx}, qf2y = {qfy, qfy}, qf2z = {qfz, qfz};
         const double bhalf = 0.5 * sqrt_up(((bx1 - bx0) * (bx1 - bx0) + (by1 - by0) * (by1 - by0)) + (bz1 - bz0) * (bz1 - bz0));
         bool seeded = false;
+#if PTV_K1_BROADCAST_SEEDS
+        if constexpr (KMAX == 1) {
+            if (a.cb.recs != nullptr) {
+                // ---- seeds (one-slot list): the 8 corners' nearest particles (lanes 0, 8, ..., 56)
+                //      broadcast to every lane; a lane's smallest distance to them bounds its nearest
+                //      neighbour.  Duplicates are harmless for a minimum: no LDS hash, no barriers ----
+                const uint32_t sl = __float_as_uint(seed.w);
+                const bool has = sl != 0xffffffffu;
+                // particle - tile centre = (particle - corner) + (corner - centre), as below
+                const float ex = seed.x + (float)(scx - tcx), ey = seed.y + (float)(scy - tcy),
+                            ez = seed.z + (float)(scz - tcz);
+                const float pm = has ? (fabsf(ex) + fabsf(ey)) + fabsf(ez) : -1.0f;
+                float best = INFINITY, pmax = -1.0f;
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                    const float sx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ex), c * 8));
+                    const float sy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ey), c * 8));
+                    const float sz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ez), c * 8));
+                    const float sp = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pm), c * 8));
+                    const float dx = qfx - sx, dy = qfy - sy, dz = qfz - sz;
+                    const float d2 = __fmaf_rn(dz, dz, __fmaf_rn(dy, dy, dx * dx));
+                    best = sp >= 0.0f ? fminf(best, d2) : best;
+                    pmax = fmaxf(pmax, sp);
+                }
+                // seed-voxel distances are <= Ms; fp32 coordinate + distance error <= Ms * 2^-19
+                const double Ms = (double)pmax * (1.0 + 1e-6) + bhalf;
+                if (active && best < INFINITY) {
+                    const double dl = Ms * 1.9073486328125e-06;
+                    const double st2 = ((double)best * (1.0 + 9.5367431640625e-07) + (2.0 * Ms * dl + dl * dl)) * (1.0 + 1e-12);
+                    if (st2 < ub2) {
+                        ub2 = st2;
+                        ub = sqrt_up(st2);
+                    }
+                }
+                if (__builtin_amdgcn_ballot_w64(active && !(best < INFINITY)) != 0) {
+                    const double u = lattice_ub();  // no corner had a record: the lattice bound
+                    if (u < ub) {
+                        ub = u;
+                        ub2 = u * u;
+                    }
+                }
+                seeded = true;
+                thr = dmin(kth2(), ub2);
+                stamp(t_seed);
+            }
+        } else
+#endif
         if constexpr (KMAX <= 8) {
             if (a.cb.recs != nullptr) {
                 // ---- seeds: the k-NN lists of the tile's 8 coarse-lattice corners.  Every lane's
