@@ -76,6 +76,9 @@ namespace ptv {
 // gains (160.9 -> 126.5) but IDW k = 60 loses (122.1 -> 130.2, 49 VGPRs spilled): 64 stays rolled.
 #define PTV_KNN_UNROLL_MAX 56
 #endif
+#ifndef PTV_VALUE_HALF_BLOCKS
+#define PTV_VALUE_HALF_BLOCKS 1  // dev builds: 0 = the value pass in whole blocks of 8
+#endif
 #ifndef PTV_KNN_KEEP_MAX
 // key lists up to this many slots keep the epilogue's distances (then weights) in registers
 // between passes; longer ones re-gather the records every pass (Sibson: four passes)
@@ -480,6 +483,31 @@ struct PairwiseStream {
 #pragma unroll
             for (int i = 0; i < 8; ++i)
                 if (m + i < n) res += a[i];
+        }
+    }
+    // the same as add(m, n, a) over the block's half h (entries m + 4h .. m + 4h + 3), both halves in
+    // order: each entry meets the same accumulator or running sum in the same order
+    __device__ __forceinline__ void add4(int m, int h, int n, const double (&a)[4]) {
+        if (n < 8) {
+            double s = h == 0 ? 0.0 : res;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (4 * h + i < n) s += a[i];
+            res = s;
+            return;
+        }
+        const int stop = n - (n & 7);
+        if (m == 0) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) r[4 * h + i] = a[i];
+        } else if (m < stop) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) r[4 * h + i] += a[i];
+        } else {
+            if (h == 0) res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (m + 4 * h + i < n) res += a[i];
         }
     }
     __device__ __forceinline__ double finish(int n) {
@@ -2057,6 +2085,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
                 tw[i] = r[2];
             }
         };
+#if PTV_VALUE_HALF_BLOCKS
+        // the 3-wave lists (KMAX <= 32): blocks in halves (spilled VGPRs at 24 / 32 slots: 30 / 98 ->
+        // 0 / 22; IDW k = 24 46.0 -> 45.0 ms, Sibson k = 30 unchanged); the 2-wave lists keep whole
+        // blocks (IDW / Sibson k = 50 +1.3 / +2.6 % in halves; profiles/r06_ab/value_half_blocks_ab.txt)
+        constexpr bool HALF = KEEP && KMAX <= 32;
+#endif
         double out[3];
         bool ok = true;
         double prev = -1.0;
@@ -2064,6 +2098,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
             // pass 1: d, 1/(d + eps) -> sum (pairwise), sum d -> mean; the order check
             PairwiseStream ps_inv, ps_d;
             double ivmin = INFINITY, dmax = 0.0, dmin_nz = INFINITY;  // operand ranges for div_by below
+#if PTV_VALUE_HALF_BLOCKS
+            if constexpr (HALF) {
+#pragma unroll
+                for (int m = 0; m < KMAX; m += 8) {
+                    if (m < k) {
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            double d2[4], dv[4], iv[4];
+                            {
+                                double4 rc[4];
+#pragma unroll
+                                for (int i = 0; i < 4; ++i) {
+                                    const int j = m + 4 * h + i;
+                                    rc[i] = prec[j < k ? slot_at(min(j, KMAX - 1)) : slot_at(0)];
+                                }
+#pragma unroll
+                                for (int i = 0; i < 4; ++i) d2[i] = exact_d2(rc[i]);
+                            }
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) {
+                                const int j = m + 4 * h + i;
+                                dv[i] = sqrt_cr(d2[i]);
+                                iv[i] = 1.0 / (dv[i] + a.eps);
+                                if (j < k) {
+                                    ok = ok && !(d2[i] < prev);
+                                    prev = d2[i];
+                                    ivmin = fmin(ivmin, iv[i]);
+                                    dmax = fmax(dmax, dv[i]);
+                                    if (dv[i] > 0.0) dmin_nz = fmin(dmin_nz, dv[i]);
+                                }
+                                if (j < KMAX) dk[min(j, KMAX - 1)] = dv[i];
+                            }
+                            ps_inv.add4(m, h, k, iv);
+                            ps_d.add4(m, h, k, dv);
+                        }
+                    }
+                }
+            } else
+#endif
 #pragma unroll
             for (int m = 0; m < KMAX; m += 8) {
                 if (m < k) {
@@ -2107,6 +2180,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
             };
             // pass 2: std (ddof 0)
             PairwiseStream ps_var;
+#if PTV_VALUE_HALF_BLOCKS
+            if constexpr (HALF) {
+#pragma unroll
+                for (int m = 0; m < KMAX; m += 8) {
+                    if (m < k) {
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            double t[4];
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) {
+                                const double c = dk[min(m + 4 * h + i, KMAX - 1)] - mean;
+                                t[i] = c * c;
+                            }
+                            ps_var.add4(m, h, k, t);
+                        }
+                    }
+                }
+            } else
+#endif
 #pragma unroll
             for (int m = 0; m < KMAX; m += 8) {
                 if (m < k) {
@@ -2140,6 +2232,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
             // register-held: pass 4 reads them back) and their sum
             PairwiseStream ps_w;
             double wmin = INFINITY;
+#if PTV_VALUE_HALF_BLOCKS
+            if constexpr (HALF) {
+#pragma unroll
+                for (int m = 0; m < KMAX; m += 8) {
+                    if (m < k) {
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            double w[4];
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) {
+                                const int j = m + 4 * h + i;
+                                const double dv = dk[min(j, KMAX - 1)];
+                                const double iv = 1.0 / (dv + a.eps);
+                                w[i] = fdiv ? div_by(iv, s_inv, rsi) * exp(div_by(-dv, den, rden))
+                                            : iv / s_inv * exp(-dv / den);
+                                if (j < k && w[i] > 0.0) wmin = fmin(wmin, w[i]);  // exp underflow: 0 / s2 exact
+                                if (j < KMAX) dk[min(j, KMAX - 1)] = w[i];
+                            }
+                            ps_w.add4(m, h, k, w);
+                        }
+                    }
+                }
+            } else
+#endif
 #pragma unroll
             for (int m = 0; m < KMAX; m += 8) {
                 if (m < k) {
@@ -2161,6 +2277,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
             const double rs2 = 1.0 / s2;
             // pass 4: normalised weights times the values
             PairwiseStream pu, pv, pw;
+#if PTV_VALUE_HALF_BLOCKS
+            if constexpr (HALF) {
+#pragma unroll
+                for (int m = 0; m < KMAX; m += 8) {
+                    if (m < k) {
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            double tu[4], tv[4], tw4[4];
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) {
+                                const int j = m + 4 * h + i;
+                                const double *r = reinterpret_cast<const double *>(
+                                    pval + (j < k ? slot_at(min(j, KMAX - 1)) : slot_at(0)));
+                                const double2 uv = *reinterpret_cast<const double2 *>(r);
+                                tu[i] = uv.x;
+                                tv[i] = uv.y;
+                                tw4[i] = r[2];
+                            }
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) {
+                                const double w = dk[min(m + 4 * h + i, KMAX - 1)];
+                                const double wn = fast ? div_by(w, s2, rs2) : w / s2;
+                                tu[i] = wn * tu[i];
+                                tv[i] = wn * tv[i];
+                                tw4[i] = wn * tw4[i];
+                            }
+                            pu.add4(m, h, k, tu);
+                            pv.add4(m, h, k, tv);
+                            pw.add4(m, h, k, tw4);
+                        }
+                    }
+                }
+            } else
+#endif
 #pragma unroll
             for (int m = 0; m < KMAX; m += 8) {
                 if (m < k) {
@@ -2191,6 +2341,41 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
             // pass 1: w = 1/(d**p + eps) -> sum (pairwise); the order check
             PairwiseStream ps;
             double wmin = INFINITY;
+#if PTV_VALUE_HALF_BLOCKS
+            if constexpr (HALF) {
+#pragma unroll
+                for (int m = 0; m < KMAX; m += 8) {
+                    if (m < k) {
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            double d2[4], w[4];
+                            {
+                                double4 rc[4];
+#pragma unroll
+                                for (int i = 0; i < 4; ++i) {
+                                    const int j = m + 4 * h + i;
+                                    rc[i] = prec[j < k ? slot_at(min(j, KMAX - 1)) : slot_at(0)];
+                                }
+#pragma unroll
+                                for (int i = 0; i < 4; ++i) d2[i] = exact_d2(rc[i]);
+                            }
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) {
+                                const int j = m + 4 * h + i;
+                                if (j < k) {
+                                    ok = ok && !(d2[i] < prev);
+                                    prev = d2[i];
+                                }
+                                if (j < KMAX) dk[min(j, KMAX - 1)] = d2[i];
+                                w[i] = 1.0 / (np_pow(sqrt_cr(d2[i]), a.power) + a.eps);
+                                if (j < k) wmin = fmin(wmin, w[i]);
+                            }
+                            ps.add4(m, h, k, w);
+                        }
+                    }
+                }
+            } else
+#endif
 #pragma unroll
             for (int m = 0; m < KMAX; m += 8) {
                 if (m < k) {
@@ -2221,6 +2406,41 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(knn_waves<K
             const double rs = 1.0 / s;
             // pass 2: normalised weights times the values
             PairwiseStream pu, pv, pw;
+#if PTV_VALUE_HALF_BLOCKS
+            if constexpr (HALF) {
+#pragma unroll
+                for (int m = 0; m < KMAX; m += 8) {
+                    if (m < k) {
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            double tu[4], tv[4], tw4[4];
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) {
+                                const int j = m + 4 * h + i;
+                                const double *r = reinterpret_cast<const double *>(
+                                    pval + (j < k ? slot_at(min(j, KMAX - 1)) : slot_at(0)));
+                                const double2 uv = *reinterpret_cast<const double2 *>(r);
+                                tu[i] = uv.x;
+                                tv[i] = uv.y;
+                                tw4[i] = r[2];
+                            }
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) {
+                                const double d2 = dk[min(m + 4 * h + i, KMAX - 1)];
+                                const double w = 1.0 / (np_pow(sqrt_cr(d2), a.power) + a.eps);
+                                const double wn = fast ? div_by(w, s, rs) : w / s;
+                                tu[i] = wn * tu[i];
+                                tv[i] = wn * tv[i];
+                                tw4[i] = wn * tw4[i];
+                            }
+                            pu.add4(m, h, k, tu);
+                            pv.add4(m, h, k, tv);
+                            pw.add4(m, h, k, tw4);
+                        }
+                    }
+                }
+            } else
+#endif
 #pragma unroll
             for (int m = 0; m < KMAX; m += 8) {
                 if (m < k) {
